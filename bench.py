@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""bench.py — decode tokens/s + achieved HBM GB/s on MI355X (BASELINE.json metric).
+
+One "step" = one greedy decode token for the B sequences a GPU holds, running the whole
+thaDNN forward (all layers, classifier, on-device argmax feeding the next token).
+Workload (N=1 line): llama2-7B-shaped fp32 model with random-init synthetic weights,
+BOS-started greedy decode over positions 0..K-1 (BASELINE.json configs[2]).
+Multi-GPU: one process per GPU (torch.distributed.run), each decodes its own independent
+prompts (weak scaling, no collective on the data path); rank 0 synthesises the weights and
+RCCL-broadcasts them over xGMI once at start-up.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model 7b|110m] [--batch B]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+MODELS = {
+    # (dim, hidden, layers, heads, kv_heads, vocab, seq_len), shared classifier
+    "7b": ((4096, 11008, 32, 32, 32, 32000, 2048), 0, "llama2-7B"),
+    "110m": ((768, 2048, 12, 12, 12, 32000, 1024), 1, "stories110M"),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=256)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--model", default="7b", choices=sorted(MODELS))
+    ap.add_argument("--batch", type=int, default=1, help="sequences per GPU")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-nt", action="store_true")
+    ap.add_argument("--splits", type=int, default=0)
+    ap.add_argument("--cpu-baseline-tokens", type=int, default=2)
+    ap.add_argument("--skip-cpu", action="store_true")
+    ap.add_argument("--prof-steps", type=int, default=16)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+    from __graft_entry__ import _pkg
+    _pkg()
+    from hip_llama_cpp_amd import thallama as tl
+
+    if tl.device_count() < 1:
+        raise SystemExit("bench.py: no HIP device")
+    torch.cuda.set_device(local)
+    tl.check(tl.lib().thallama_set_device(local))
+    if world > 1:
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+
+    cfg_t, shared, mname = MODELS[args.model]
+    c = tl.Config.make(*cfg_t)
+    B, K, W = args.batch, args.steps, args.warmup
+    S = cfg_t[6]
+    if K > S or W > S:
+        raise SystemExit(f"--steps/--warmup must be <= seq_len {S}")
+
+    # ---------------- weights: one arena, rank 0 synthesises, RCCL broadcast to the others
+    n_floats = tl.lib().thallama_v0_payload_floats(tl.C.byref(c), shared)
+    t0 = time.perf_counter()
+    arena = torch.empty(n_floats, dtype=torch.float32, device=f"cuda:{local}")
+    if rank == 0 or world == 1:
+        tl.check(tl.lib().thallama_synth_arena(tl.C.cast(tl.C.c_void_p(arena.data_ptr()), tl.c_float_p),
+                                               tl.C.byref(c), shared, tl.C.c_uint64(20240224), None), "synth")
+    torch.cuda.synchronize()
+    t_bcast = 0.0
+    if world > 1:
+        dist.barrier()
+        tb = time.perf_counter()
+        chunk = 1 << 28  # 1 GiB of fp32 per collective
+        for s in range(0, n_floats, chunk):
+            dist.broadcast(arena[s:s + chunk], src=0)
+        torch.cuda.synchronize()
+        t_bcast = time.perf_counter() - tb
+    t_init = time.perf_counter() - t0
+    model = tl.DeviceModel(c, shared, arena_ptr=arena.data_ptr())
+    state = tl.DeviceState(c, B)
+    dec = tl.Decoder(model, state)
+    dec.set(tl.OPT_USE_GRAPH, 0 if args.no_graph else 1)
+    if args.no_nt:
+        dec.set(tl.OPT_NT_WEIGHTS, 0)
+    if args.splits:
+        dec.set(tl.OPT_ATTN_SPLITS, args.splits)
+    log(f"[rank {rank}] model {mname} B={B} init {t_init:.2f}s (broadcast {t_bcast:.2f}s)")
+
+    tok0 = [1] * B  # BOS
+    pos0 = [0] * B
+    # ---------------- warmup
+    if W:
+        dec.greedy(tok0, pos0, W, want_tokens=False, sync=True)
+    # ---------------- timed region: K greedy steps at positions 0..K-1
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    dec.greedy(tok0, pos0, K, want_tokens=False, sync=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    tokens = world * B * K
+    value = tokens / elapsed
+    ms_step = elapsed / K * 1e3
+
+    # whole-step algorithmic bytes (weights once per step + KV read/written at each position)
+    positions = list(range(K))
+    step_bytes = 0.0
+    for p in positions:
+        pos = [p] * B
+        L = cfg_t[2]
+        step_bytes += L * sum(tl.step_bytes(c, B, k, pos) for k in (tl.K_QKV, tl.K_ATTN, tl.K_WO, tl.K_FFN_UP,
+                                                                      tl.K_FFN_DOWN))
+        step_bytes += tl.step_bytes(c, B, tl.K_CLS, pos) + tl.step_bytes(c, B, tl.K_ARGMAX, pos)
+    step_bytes /= K
+    step_gbs = step_bytes / (ms_step * 1e-3) / 1e9
+
+    # ---------------- dominant-kernel roofline: HIP events around every launch (eager replay of
+    # the same steps on the decoder's stream), averaged per kernel class
+    prof = {}
+    if rank == 0:
+        P = min(args.prof_steps, K)
+        dec.set(tl.OPT_PROFILE, 1)
+        dec.prof_reset()
+        dec.greedy(tok0, pos0, P, want_tokens=False, sync=True)
+        for k, name in enumerate(tl.K_NAMES):
+            ms, n = dec.prof(k)
+            if n:
+                prof[name] = {"avg_us": 1e3 * ms / n, "launches": n}
+        dec.set(tl.OPT_PROFILE, 0)
+        ffn = prof.get("ffn_up", {})
+        bytes_ffn = tl.step_bytes(c, B, tl.K_FFN_UP, [0] * B)
+        if ffn:
+            prof["ffn_up"]["GBps"] = bytes_ffn / (ffn["avg_us"] * 1e-6) / 1e9
+        for name, k in (("qkv", tl.K_QKV), ("wo", tl.K_WO), ("ffn_down", tl.K_FFN_DOWN), ("cls", tl.K_CLS)):
+            if name in prof:
+                prof[name]["GBps"] = tl.step_bytes(c, B, k, [0] * B) / (prof[name]["avg_us"] * 1e-6) / 1e9
+
+    # ---------------- CPU baseline: the oracle's seq.cpp restatement, 1 core, same model shape
+    cpu = None
+    if rank == 0 and world == 1 and not args.skip_cpu and args.cpu_baseline_tokens > 0:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle as O
+        O.set_threads(min(16, os.cpu_count() or 1))  # weight synthesis only
+        ref = O.Model(cfg_t, shared, seed=20240224)
+        O.set_threads(1)
+        n = args.cpu_baseline_tokens
+        tc = time.perf_counter()
+        ctoks = ref.greedy(1, 0, n)
+        tcpu = time.perf_counter() - tc
+        gtoks = dec.greedy(tok0[:1] * B, pos0, n)[:, 0].tolist()
+        cpu = {"value": n / tcpu, "unit": "tok/s", "cores": 1, "kind": "port",
+               "sample": f"{n} greedy tokens from BOS (pos 0..{n - 1}) of the same synthetic {mname} fp32 model, "
+                         f"oracle/oracle.c (bit-exact seq.cpp restatement), single thread",
+               "tokens_match_gpu": ctoks == gtoks}
+        ref.close()
+
+    if rank == 0:
+        ffn = prof.get("ffn_up")
+        roof = None
+        if ffn:
+            achieved = ffn["GBps"]
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "kernel": "gemv_kernel<GM_SWIGLU> (RMSNorm + W1/W3 + SwiGLU)",
+                    "bytes_per_launch": tl.step_bytes(c, B, tl.K_FFN_UP, [0] * B),
+                    "avg_us": round(ffn["avg_us"], 2)}
+        out = {
+            "metric": "decode tokens/sec (greedy, whole model) + achieved HBM GB/s fraction",
+            "value": round(value, 3), "unit": "tok/s", "n_gpus": world, "steps": K, "warmup": W,
+            "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic (random-init weights, BOS-started greedy)",
+            "config": {"workload": f"{mname} fp32 decode, {B} seq/GPU, positions 0..{K - 1}", "model": mname,
+                       "global_batch": B * world, "seq_len": S, "parallelism": f"prompt-dp{world}"},
+            "hbm": {"step_bytes": step_bytes, "achieved_GBps": round(step_gbs, 1),
+                    "frac_of_peak": round(step_gbs / HBM_PEAK_GBS, 4),
+                    "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / step_bytes * B * world, 1)},
+            "roofline": roof,
+            "kernels": {k: {kk: round(vv, 2) for kk, vv in v.items()} for k, v in prof.items()},
+            "cpu_baseline": cpu,
+            "init_s": round(t_init, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

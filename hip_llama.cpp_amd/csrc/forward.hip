@@ -1,0 +1,572 @@
+// forward.hip — the fused decode step (thaDNN_s_forward_batch) and the native decoder.
+//
+// Reference: src/thaDNN.cpp:13-81 issues, per layer, 9 + 4*B launches (RMSNorm,
+// 7 GEMVs that each re-read the weights once per sequence, per-sequence RoPE /
+// residual / SwiGLU launches, 3 attention kernels) plus a hipMalloc/hipFree and
+// B blocking D2D copies per step.  Here one step is, per layer:
+//
+//   1. QKV    : RMSNorm(att) prologue + [Wq;Wk;Wv] GEMV + RoPE + KV-cache write
+//               (layer 0 also folds the embedding lookup)
+//   2. ATTN   : scores + softmax + V-sum, one launch (+ combine when keys split)
+//   3. WO     : Wo GEMV + residual add
+//   4. FFN_UP : RMSNorm(ffn) prologue + [W1;W3] GEMV + SwiGLU
+//   5. FFN_DN : W2 GEMV + residual add
+//
+// then RMSNorm(final) + classifier, and (greedy loop only) an argmax that feeds
+// the next token and position back on the device.  Every launch reads every
+// weight byte once for all B sequences.  Nothing allocates or synchronises
+// inside a step, so a step can be captured into a hipGraph.
+#include <math.h>
+#include <string.h>
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+#include <string>
+#include "../../include/thaDNN.hpp"
+#include "../../include/thallama.h"
+#include "../../include/hip_helper.hpp"
+#include "attention.hpp"
+#include "gemv_dispatch.hpp"
+
+using tl::f4;
+
+static thread_local std::string g_last_error;
+extern "C" const char* thallama_last_error(void) { return g_last_error.c_str(); }
+
+#define TL_TRY(cmd)                                                                   \
+  do {                                                                                \
+    hipError_t e_ = (cmd);                                                            \
+    if (e_ != hipSuccess) {                                                           \
+      g_last_error = std::string(#cmd) + ": " + hipGetErrorString(e_) + " @" +        \
+                     std::to_string(__LINE__);                                        \
+      return (int)e_;                                                                 \
+    }                                                                                 \
+  } while (0)
+
+// ------------------------------------------------------------------ argmax + advance
+// next = argmax(logits[b]) with lowest-index ties (sample_argmax, reference
+// src/llama.cpp:275-286); then tok[b] = next, out[b*cap + pos[b]] = next, pos[b]++.
+__global__ void __launch_bounds__(256) k_argmax_advance(const float* logits, int V, int* tok, int* pos,
+                                                        int* out, int cap) {
+  __shared__ unsigned long long red[4];
+  const int b = blockIdx.x;
+  const float* l = logits + (long long)b * V;
+  unsigned long long best = 0;
+  for (int i = threadIdx.x; i < V; i += 256) {
+    unsigned long long k = tl::argmax_pack(l[i], i);
+    best = k > best ? k : best;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long other = __shfl_xor(best, o, 64);
+    best = other > best ? other : best;
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) best = red[w] > best ? red[w] : best;
+    const int next = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
+    const int p = pos[b];
+    if (out && p < cap) out[(long long)b * cap + p] = next;
+    tok[b] = next;
+    pos[b] = p + 1;
+  }
+}
+
+// ------------------------------------------------------------------ decoder
+struct thallama_decoder {
+  Config cfg;
+  TransformerWeights w;
+  RunState s;
+  int B = 1;
+  int dev = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  int dim, hidden, L, H, kv_dim, kv_mul, hs, V, S;
+  // workspace
+  int* tok_d = nullptr;
+  int* pos_d = nullptr;
+  int* out_d = nullptr;  // [B][S] greedy tokens by position
+  int* tok_h = nullptr;  // pinned staging
+  int* pos_h = nullptr;
+  float2* rope_d = nullptr;
+  float* part_d = nullptr;
+  int nsplit = 1;
+  bool nt = true;
+  bool use_graph = false;
+  bool profile = false;
+  hipGraphExec_t exec = nullptr;
+  // profiling
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<int, int>> ev_marks;  // (class, event index of start)
+  size_t ev_next = 0;
+  double prof_ms[THALLAMA_K_COUNT] = {0};
+  long long prof_n[THALLAMA_K_COUNT] = {0};
+};
+
+static int prof_begin(thallama_decoder* d) {
+  if (!d->profile) return -1;
+  if (d->ev_next + 2 > d->ev_pool.size()) {
+    for (int i = 0; i < 512; ++i) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return -1;
+      d->ev_pool.push_back(e);
+    }
+  }
+  int i = (int)d->ev_next;
+  d->ev_next += 2;
+  (void)hipEventRecord(d->ev_pool[i], d->stream);
+  return i;
+}
+
+static void prof_end(thallama_decoder* d, int kclass, int i) {
+  if (i < 0) return;
+  (void)hipEventRecord(d->ev_pool[i + 1], d->stream);
+  d->ev_marks.push_back({kclass, i});
+}
+
+static void prof_collect(thallama_decoder* d) {
+  if (d->ev_marks.empty()) return;
+  (void)hipStreamSynchronize(d->stream);
+  for (auto& m : d->ev_marks) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, d->ev_pool[m.second], d->ev_pool[m.second + 1]) == hipSuccess) {
+      d->prof_ms[m.first] += ms;
+      d->prof_n[m.first] += 1;
+    }
+  }
+  d->ev_marks.clear();
+  d->ev_next = 0;
+}
+
+static int auto_splits(const thallama_decoder* d) {
+  // Enough (head, seq, split) blocks to cover the 256 CUs, at most 16 splits.
+  int blocks = d->H * d->B;
+  int ns = (256 + blocks - 1) / blocks;
+  if (ns < 1) ns = 1;
+  if (ns > 16) ns = 16;
+  return ns;
+}
+
+extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg, const TransformerWeights* w,
+                                       const RunState* s, int batch, hipStream_t stream) {
+  if (!out || !cfg || !w || !s || batch <= 0) {
+    g_last_error = "thallama_decoder_create: invalid argument";
+    return (int)hipErrorInvalidValue;
+  }
+  const Config& c = *cfg;
+  if (c.dim <= 0 || c.n_heads <= 0 || c.n_kv_heads <= 0 || c.dim % c.n_heads || c.n_heads % c.n_kv_heads ||
+      (c.dim / c.n_heads) % 8 || (c.dim / c.n_heads) > 512 || c.seq_len <= 0) {
+    g_last_error = "thallama_decoder_create: unsupported config (head_size must be a multiple of 8, <= 512)";
+    return (int)hipErrorInvalidValue;
+  }
+  thallama_decoder* d = new thallama_decoder();
+  d->cfg = c;
+  d->cfg.vocab_size = c.vocab_size < 0 ? -c.vocab_size : c.vocab_size;
+  d->w = *w;
+  d->s = *s;
+  d->B = batch;
+  d->dim = c.dim;
+  d->hidden = c.hidden_dim;
+  d->L = c.n_layers;
+  d->H = c.n_heads;
+  d->hs = c.dim / c.n_heads;
+  d->kv_dim = c.dim * c.n_kv_heads / c.n_heads;
+  d->kv_mul = c.n_heads / c.n_kv_heads;
+  d->V = d->cfg.vocab_size;
+  d->S = c.seq_len;
+  TL_TRY(hipGetDevice(&d->dev));
+  if (stream) {
+    d->stream = stream;
+  } else {
+    TL_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    d->own_stream = true;
+  }
+  TL_TRY(hipMalloc(&d->tok_d, sizeof(int) * batch));
+  TL_TRY(hipMalloc(&d->pos_d, sizeof(int) * batch));
+  TL_TRY(hipMalloc(&d->out_d, sizeof(int) * (size_t)batch * d->S));
+  TL_TRY(hipHostMalloc(&d->tok_h, sizeof(int) * batch, hipHostMallocDefault));
+  TL_TRY(hipHostMalloc(&d->pos_h, sizeof(int) * batch, hipHostMallocDefault));
+  // RoPE table with the reference's exact host formula (src/seq.cpp:88-92), so the
+  // device rotation uses bit-identical cos/sin.
+  std::vector<float2> rope((size_t)d->S * (d->hs / 2));
+  for (int p = 0; p < d->S; ++p)
+    for (int hd = 0; hd < d->hs; hd += 2) {
+      float freq = 1.0f / powf(10000.0f, hd / (float)d->hs);
+      float val = p * freq;
+      rope[(size_t)p * (d->hs / 2) + hd / 2] = make_float2(cosf(val), sinf(val));
+    }
+  TL_TRY(hipMalloc(&d->rope_d, rope.size() * sizeof(float2)));
+  TL_TRY(hipMemcpy(d->rope_d, rope.data(), rope.size() * sizeof(float2), hipMemcpyHostToDevice));
+  d->nsplit = auto_splits(d);
+  TL_TRY(hipMalloc(&d->part_d, sizeof(float) * (size_t)batch * d->H * 16 * (d->hs + 4)));
+  // weights far beyond the 256 MiB Infinity Cache stream once per step: nt loads
+  const double wbytes = 4.0 * ((double)d->L * (2.0 * d->dim * d->dim + 2.0 * d->dim * d->kv_dim +
+                                               3.0 * d->dim * d->hidden) + (double)d->V * d->dim);
+  d->nt = wbytes > 1024.0 * 1024.0 * 1024.0;
+  *out = d;
+  return 0;
+}
+
+extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
+  if (!d) return;
+  (void)hipStreamSynchronize(d->stream);
+  if (d->exec) (void)hipGraphExecDestroy(d->exec);
+  for (auto e : d->ev_pool) (void)hipEventDestroy(e);
+  (void)hipFree(d->tok_d);
+  (void)hipFree(d->pos_d);
+  (void)hipFree(d->out_d);
+  (void)hipHostFree(d->tok_h);
+  (void)hipHostFree(d->pos_h);
+  (void)hipFree(d->rope_d);
+  (void)hipFree(d->part_d);
+  if (d->own_stream) (void)hipStreamDestroy(d->stream);
+  delete d;
+}
+
+extern "C" int thallama_decoder_set(thallama_decoder* d, int key, int value) {
+  if (!d) return (int)hipErrorInvalidValue;
+  switch (key) {
+    case THALLAMA_OPT_NT_WEIGHTS: d->nt = value != 0; break;
+    case THALLAMA_OPT_ATTN_SPLITS: d->nsplit = value <= 0 ? auto_splits(d) : (value > 16 ? 16 : value); break;
+    case THALLAMA_OPT_USE_GRAPH: d->use_graph = value != 0; break;
+    case THALLAMA_OPT_PROFILE: d->profile = value != 0; break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  if (d->exec) {  // options are baked into a captured graph: recapture on next use
+    (void)hipGraphExecDestroy(d->exec);
+    d->exec = nullptr;
+  }
+  return 0;
+}
+
+extern "C" hipStream_t thallama_decoder_stream(thallama_decoder* d) { return d ? d->stream : nullptr; }
+
+// Enqueue one decode step reading tok_d / pos_d; logits land in s.logits.
+static int enqueue_step(thallama_decoder* d) {
+  const int dim = d->dim, hid = d->hidden, kvd = d->kv_dim, S = d->S;
+  const long long kv_b_stride = (long long)d->L * S * kvd;
+  const TransformerWeights& w = d->w;
+  const RunState& s = d->s;
+  for (int l = 0; l < d->L; ++l) {
+    const long long ll = l;
+    // 1. QKV (+ embedding at layer 0)
+    {
+      tl::GemvParams p = {};
+      p.W0 = w.wq + ll * dim * dim;
+      p.W1 = w.wk + ll * dim * kvd;
+      p.W2 = w.wv + ll * dim * kvd;
+      p.K = dim;
+      p.n_items = (dim + 2 * kvd) / 2;
+      p.nb = d->B;
+      p.x = s.x;
+      p.x_stride = dim;
+      p.rms_w = w.rms_att_weight + ll * dim;
+      if (l == 0) {
+        p.tok = d->tok_d;
+        p.emb = w.token_embedding_table;
+        p.x_out = s.x;
+      }
+      p.y = s.q;
+      p.y_stride = dim;
+      p.pos = d->pos_d;
+      p.kc = s.key_cache;
+      p.vc = s.value_cache;
+      p.kv_b_stride = kv_b_stride;
+      p.kv_l_off = ll * S * kvd;
+      p.dim = dim;
+      p.kv_dim = kvd;
+      p.head_size = d->hs;
+      p.rope = d->rope_d;
+      int ev = prof_begin(d);
+      TL_TRY(tl::launch_gemv(tl::GM_QKV, p, d->stream, d->nt));
+      prof_end(d, THALLAMA_K_QKV, ev);
+    }
+    // 2. attention
+    {
+      tl::AttnParams a = {};
+      a.q = s.q;
+      a.kc = s.key_cache;
+      a.vc = s.value_cache;
+      a.kv_b_stride = kv_b_stride;
+      a.kv_l_off = ll * S * kvd;
+      a.pos = d->pos_d;
+      a.out = s.xb;
+      a.part = d->part_d;
+      a.dim = dim;
+      a.kv_dim = kvd;
+      a.head_size = d->hs;
+      a.n_heads = d->H;
+      a.kv_mul = d->kv_mul;
+      a.seq_len = S;
+      a.nsplit = d->nsplit;
+      a.min_chunk = 32;
+      const int lpk = d->hs / 4;
+      const size_t lds = 64 + (size_t)(S > 1024 ? S : 1024) * 4;
+      int ev = prof_begin(d);
+      dim3 grid(d->H, d->B, d->nsplit);
+      switch (lpk) {
+        case 2: hipLaunchKernelGGL(tl::attn_decode_kernel<2>, grid, dim3(256), lds, d->stream, a); break;
+        case 4: hipLaunchKernelGGL(tl::attn_decode_kernel<4>, grid, dim3(256), lds, d->stream, a); break;
+        case 8: hipLaunchKernelGGL(tl::attn_decode_kernel<8>, grid, dim3(256), lds, d->stream, a); break;
+        case 16: hipLaunchKernelGGL(tl::attn_decode_kernel<16>, grid, dim3(256), lds, d->stream, a); break;
+        case 32: hipLaunchKernelGGL(tl::attn_decode_kernel<32>, grid, dim3(256), lds, d->stream, a); break;
+        case 64: hipLaunchKernelGGL(tl::attn_decode_kernel<64>, grid, dim3(256), lds, d->stream, a); break;
+        default:
+          g_last_error = "unsupported head_size for fused attention";
+          return (int)hipErrorInvalidValue;
+      }
+      TL_TRY(hipGetLastError());
+      if (d->nsplit > 1) {
+        hipLaunchKernelGGL(tl::attn_combine_kernel, dim3(d->H, d->B), dim3(128), 0, d->stream, a);
+        TL_TRY(hipGetLastError());
+      }
+      prof_end(d, THALLAMA_K_ATTN, ev);
+    }
+    // 3. Wo + residual
+    {
+      tl::GemvParams p = {};
+      p.W0 = w.wo + ll * dim * dim;
+      p.K = dim;
+      p.n_items = dim;
+      p.nb = d->B;
+      p.x = s.xb;
+      p.x_stride = dim;
+      p.y = s.x;
+      p.y_stride = dim;
+      int ev = prof_begin(d);
+      TL_TRY(tl::launch_gemv(tl::GM_RESID, p, d->stream, d->nt));
+      prof_end(d, THALLAMA_K_WO, ev);
+    }
+    // 4. RMSNorm(ffn) + W1/W3 + SwiGLU
+    {
+      tl::GemvParams p = {};
+      p.W0 = w.w1 + ll * dim * hid;
+      p.W1 = w.w3 + ll * dim * hid;
+      p.K = dim;
+      p.n_items = hid;
+      p.nb = d->B;
+      p.x = s.x;
+      p.x_stride = dim;
+      p.rms_w = w.rms_ffn_weight + ll * dim;
+      p.y = s.hb;
+      p.y_stride = hid;
+      int ev = prof_begin(d);
+      TL_TRY(tl::launch_gemv(tl::GM_SWIGLU, p, d->stream, d->nt));
+      prof_end(d, THALLAMA_K_FFN_UP, ev);
+    }
+    // 5. W2 + residual
+    {
+      tl::GemvParams p = {};
+      p.W0 = w.w2 + ll * dim * hid;
+      p.K = hid;
+      p.n_items = dim;
+      p.nb = d->B;
+      p.x = s.hb;
+      p.x_stride = hid;
+      p.y = s.x;
+      p.y_stride = dim;
+      int ev = prof_begin(d);
+      TL_TRY(tl::launch_gemv(tl::GM_RESID, p, d->stream, d->nt));
+      prof_end(d, THALLAMA_K_FFN_DOWN, ev);
+    }
+  }
+  // final RMSNorm + classifier
+  {
+    tl::GemvParams p = {};
+    p.W0 = w.wcls;
+    p.K = dim;
+    p.n_items = d->V;
+    p.nb = d->B;
+    p.x = s.x;
+    p.x_stride = dim;
+    p.rms_w = w.rms_final_weight;
+    if (d->L == 0) {
+      p.tok = d->tok_d;
+      p.emb = w.token_embedding_table;
+      p.x_out = s.x;
+    }
+    p.y = s.logits;
+    p.y_stride = d->V;
+    int ev = prof_begin(d);
+    TL_TRY(tl::launch_gemv(tl::GM_STORE, p, d->stream, d->nt));
+    prof_end(d, THALLAMA_K_CLS, ev);
+  }
+  return 0;
+}
+
+static int enqueue_argmax(thallama_decoder* d) {
+  int ev = prof_begin(d);
+  hipLaunchKernelGGL(k_argmax_advance, dim3(d->B), dim3(256), 0, d->stream, d->s.logits, d->V, d->tok_d,
+                     d->pos_d, d->out_d, d->S);
+  TL_TRY(hipGetLastError());
+  prof_end(d, THALLAMA_K_ARGMAX, ev);
+  return 0;
+}
+
+static int upload_tok_pos(thallama_decoder* d, const int* token_h, const int* pos_h) {
+  for (int b = 0; b < d->B; ++b) {
+    if (pos_h[b] < 0 || pos_h[b] >= d->S || token_h[b] < 0 || token_h[b] >= d->V) {
+      g_last_error = "token/pos out of range";
+      return (int)hipErrorInvalidValue;
+    }
+  }
+  // the staging buffers may still feed an in-flight copy of the previous call
+  TL_TRY(hipStreamSynchronize(d->stream));
+  memcpy(d->tok_h, token_h, sizeof(int) * d->B);
+  memcpy(d->pos_h, pos_h, sizeof(int) * d->B);
+  TL_TRY(hipMemcpyAsync(d->tok_d, d->tok_h, sizeof(int) * d->B, hipMemcpyHostToDevice, d->stream));
+  TL_TRY(hipMemcpyAsync(d->pos_d, d->pos_h, sizeof(int) * d->B, hipMemcpyHostToDevice, d->stream));
+  return 0;
+}
+
+extern "C" int thallama_decoder_forward(thallama_decoder* d, const int* token_h, const int* pos_h, float* logits_h) {
+  if (!d || !token_h || !pos_h) return (int)hipErrorInvalidValue;
+  int r = upload_tok_pos(d, token_h, pos_h);
+  if (r) return r;
+  r = enqueue_step(d);
+  if (r) return r;
+  if (logits_h)
+    TL_TRY(hipMemcpyAsync(logits_h, d->s.logits, sizeof(float) * (size_t)d->B * d->V, hipMemcpyDeviceToHost,
+                          d->stream));
+  TL_TRY(hipStreamSynchronize(d->stream));
+  prof_collect(d);
+  return 0;
+}
+
+extern "C" int thallama_decoder_greedy(thallama_decoder* d, const int* token0_h, const int* pos0_h, int n_steps,
+                                       int* tokens_out_h, int sync) {
+  if (!d || !token0_h || !pos0_h || n_steps < 0) return (int)hipErrorInvalidValue;
+  for (int b = 0; b < d->B; ++b)
+    if (pos0_h[b] + n_steps > d->S) {
+      g_last_error = "greedy decode would run past seq_len";
+      return (int)hipErrorInvalidValue;
+    }
+  int r = upload_tok_pos(d, token0_h, pos0_h);
+  if (r) return r;
+  const bool graph = d->use_graph && !d->profile;
+  if (graph && !d->exec) {
+    hipGraph_t g = nullptr;
+    TL_TRY(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
+    int e = enqueue_step(d);
+    if (!e) e = enqueue_argmax(d);
+    hipError_t ce = hipStreamEndCapture(d->stream, &g);
+    if (e) return e;
+    TL_TRY(ce);
+    TL_TRY(hipGraphInstantiate(&d->exec, g, nullptr, nullptr, 0));
+    (void)hipGraphDestroy(g);
+  }
+  for (int i = 0; i < n_steps; ++i) {
+    if (graph) {
+      TL_TRY(hipGraphLaunch(d->exec, d->stream));
+    } else {
+      r = enqueue_step(d);
+      if (r) return r;
+      r = enqueue_argmax(d);
+      if (r) return r;
+    }
+  }
+  if (tokens_out_h && n_steps > 0) {
+    // tokens by position: sequence b generated out[b][pos0+1 .. pos0+n_steps] ... stored at pos index
+    std::vector<int> tmp((size_t)d->B * d->S);
+    TL_TRY(hipMemcpyAsync(tmp.data(), d->out_d, sizeof(int) * tmp.size(), hipMemcpyDeviceToHost, d->stream));
+    TL_TRY(hipStreamSynchronize(d->stream));
+    for (int i = 0; i < n_steps; ++i)
+      for (int b = 0; b < d->B; ++b) tokens_out_h[(size_t)i * d->B + b] = tmp[(size_t)b * d->S + pos0_h[b] + i];
+  } else if (sync) {
+    TL_TRY(hipStreamSynchronize(d->stream));
+  }
+  prof_collect(d);
+  return 0;
+}
+
+extern "C" int thallama_decoder_logits(thallama_decoder* d, float* logits_h) {
+  if (!d || !logits_h) return (int)hipErrorInvalidValue;
+  TL_TRY(hipMemcpyAsync(logits_h, d->s.logits, sizeof(float) * (size_t)d->B * d->V, hipMemcpyDeviceToHost,
+                        d->stream));
+  TL_TRY(hipStreamSynchronize(d->stream));
+  return 0;
+}
+
+extern "C" int thallama_decoder_prof(thallama_decoder* d, int kclass, double* total_ms, long long* count) {
+  if (!d || kclass < 0 || kclass >= THALLAMA_K_COUNT) return (int)hipErrorInvalidValue;
+  prof_collect(d);
+  if (total_ms) *total_ms = d->prof_ms[kclass];
+  if (count) *count = d->prof_n[kclass];
+  return 0;
+}
+
+extern "C" void thallama_decoder_prof_reset(thallama_decoder* d) {
+  if (!d) return;
+  prof_collect(d);
+  for (int i = 0; i < THALLAMA_K_COUNT; ++i) {
+    d->prof_ms[i] = 0;
+    d->prof_n[i] = 0;
+  }
+}
+
+extern "C" double thallama_step_bytes(const Config* c, int B, int kclass, const int* pos_h) {
+  const double dim = c->dim, hid = c->hidden_dim, V = c->vocab_size < 0 ? -c->vocab_size : c->vocab_size;
+  const double kvd = (double)c->dim * c->n_kv_heads / c->n_heads;
+  switch (kclass) {
+    case THALLAMA_K_QKV: return 4.0 * ((dim * dim + 2 * dim * kvd) + dim + B * (dim + dim + 2 * kvd));
+    case THALLAMA_K_ATTN: {
+      double t = 0;
+      for (int b = 0; b < B; ++b) t += (pos_h ? pos_h[b] + 1 : 1);
+      return 4.0 * (2 * kvd * t + B * 2 * dim);
+    }
+    case THALLAMA_K_WO: return 4.0 * (dim * dim + B * 3 * dim);
+    case THALLAMA_K_FFN_UP: return 4.0 * (2 * hid * dim + dim + B * (dim + hid));
+    case THALLAMA_K_FFN_DOWN: return 4.0 * (hid * dim + B * (hid + 2 * dim));
+    case THALLAMA_K_CLS: return 4.0 * (V * dim + dim + B * (dim + V));
+    case THALLAMA_K_ARGMAX: return 4.0 * B * V;
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------ thaDNN_s_forward_batch
+// The reference signature carries no workspace, so one decoder per
+// (device, stream, weights, state, batch, config) is created on first use and reused.
+namespace {
+typedef std::tuple<int, hipStream_t, const void*, const void*, const void*, int, int, int, int, int> DecKey;
+std::mutex g_dec_mu;
+std::map<DecKey, thallama_decoder*>& dec_cache() {
+  static std::map<DecKey, thallama_decoder*> m;
+  return m;
+}
+}  // namespace
+
+extern "C" thablasStatus_t thaDNN_s_forward_batch(thablasHandle_t handle1, thablasHandle_t handle2,
+                                                  thablasHandle_t handle3, int n_batches, Config* p,
+                                                  TransformerWeights* w, RunState* s_batch, int token[],
+                                                  int pos[], float* logits_host) {
+  (void)handle2;
+  (void)handle3;
+  if (!p || !w || !s_batch || !token || !pos || !logits_host || n_batches <= 0) return THABLAS_STATUS_INVALID_VALUE;
+  int dev = 0;
+  CHECK_HIP(hipGetDevice(&dev));
+  DecKey key(dev, handle1.calc_stream, (const void*)w->wq, (const void*)s_batch->key_cache,
+             (const void*)s_batch->x, n_batches, p->dim, p->n_layers, p->seq_len, p->vocab_size);
+  thallama_decoder* d = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_dec_mu);
+    auto it = dec_cache().find(key);
+    if (it != dec_cache().end()) {
+      d = it->second;
+      d->w = *w;
+      d->s = *s_batch;
+    } else {
+      if (thallama_decoder_create(&d, p, w, s_batch, n_batches, handle1.calc_stream) != 0) {
+        fprintf(stderr, "thaDNN_s_forward_batch: %s\n", thallama_last_error());
+        return THABLAS_STATUS_INVALID_VALUE;
+      }
+      dec_cache()[key] = d;
+    }
+  }
+  int r = thallama_decoder_forward(d, token, pos, logits_host);
+  if (r) {
+    fprintf(stderr, "thaDNN_s_forward_batch: %s\n", thallama_last_error());
+    return r == (int)hipErrorInvalidValue ? THABLAS_STATUS_INVALID_VALUE : THABLAS_STATUS_EXECUTION_FAILED;
+  }
+  return THABLAS_STATUS_SUCCESS;
+}

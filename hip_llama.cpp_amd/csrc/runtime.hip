@@ -1,0 +1,266 @@
+// runtime.hip — model.bin v0 loader, device residency, synthetic weights and
+// small device-memory helpers.
+//
+// Loader semantics follow the reference exactly (src/utils.cpp:119-177:
+// 28-byte Config header, negative vocab_size = unshared classifier, mmap,
+// v0 tensor order, freq_cis block skipped).  Device residency differs by
+// design: the reference issues 12 hipMalloc + 12 blocking H2D copies per GPU
+// (src/models.cpp:86-125); here the payload is ONE arena with the file's own
+// layout, so upload is one copy and replication to other GPUs is one RCCL
+// broadcast (apps/batch_manager.cpp).
+#include <fcntl.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <unistd.h>
+#include "../../include/hip_helper.hpp"
+#include "../../include/thallama.h"
+#include "synth.hpp"
+
+// ------------------------------------------------------------------ layout
+extern "C" size_t thallama_v0_payload_floats(const Config* p, int shared_weights) {
+  const size_t dim = p->dim, hid = p->hidden_dim, L = p->n_layers, V = p->vocab_size < 0 ? -p->vocab_size : p->vocab_size;
+  const size_t hs = p->dim / p->n_heads, kvd = (size_t)p->dim * p->n_kv_heads / p->n_heads;
+  size_t n = V * dim;              // token_embedding_table
+  n += L * dim;                    // rms_att
+  n += L * dim * dim;              // wq
+  n += 2 * L * dim * kvd;          // wk, wv
+  n += L * dim * dim;              // wo
+  n += L * dim;                    // rms_ffn
+  n += 3 * L * dim * hid;          // w1, w2, w3
+  n += dim;                        // rms_final
+  n += (size_t)p->seq_len * hs;    // freq_cis_real + freq_cis_imag (unused)
+  if (!shared_weights) n += V * dim;
+  return n;
+}
+
+// reference src/utils.cpp:119-148
+extern "C" void thallama_map_weights(TransformerWeights* w, const Config* p, float* ptr, int shared_weights) {
+  const int head_size = p->dim / p->n_heads;
+  const unsigned long long n_layers = p->n_layers;
+  const unsigned long long V = p->vocab_size < 0 ? -p->vocab_size : p->vocab_size;
+  w->token_embedding_table = ptr;
+  ptr += V * p->dim;
+  w->rms_att_weight = ptr;
+  ptr += n_layers * p->dim;
+  w->wq = ptr;
+  ptr += n_layers * p->dim * (p->n_heads * head_size);
+  w->wk = ptr;
+  ptr += n_layers * p->dim * (p->n_kv_heads * head_size);
+  w->wv = ptr;
+  ptr += n_layers * p->dim * (p->n_kv_heads * head_size);
+  w->wo = ptr;
+  ptr += n_layers * (p->n_heads * head_size) * p->dim;
+  w->rms_ffn_weight = ptr;
+  ptr += n_layers * p->dim;
+  w->w1 = ptr;
+  ptr += n_layers * p->dim * p->hidden_dim;
+  w->w2 = ptr;
+  ptr += n_layers * p->hidden_dim * p->dim;
+  w->w3 = ptr;
+  ptr += n_layers * p->dim * p->hidden_dim;
+  w->rms_final_weight = ptr;
+  ptr += p->dim;
+  ptr += (unsigned long long)p->seq_len * head_size / 2;
+  ptr += (unsigned long long)p->seq_len * head_size / 2;
+  w->wcls = shared_weights ? w->token_embedding_table : ptr;
+}
+
+extern "C" void memory_map_weights(TransformerWeights* w, Config* p, float* ptr, int shared_weights) {
+  thallama_map_weights(w, p, ptr, shared_weights);
+}
+
+// ------------------------------------------------------------------ host loader
+// reference src/utils.cpp:85-104
+extern "C" void malloc_run_state(RunState* s, Config* p) {
+  const int kv_dim = (p->dim * p->n_kv_heads) / p->n_heads;
+  memset(s, 0, sizeof(*s));
+  s->x = (float*)calloc(p->dim, sizeof(float));
+  s->xb = (float*)calloc(p->dim, sizeof(float));
+  s->xb2 = (float*)calloc(p->dim, sizeof(float));
+  s->hb = (float*)calloc(p->hidden_dim, sizeof(float));
+  s->hb2 = (float*)calloc(p->hidden_dim, sizeof(float));
+  s->q = (float*)calloc(p->dim, sizeof(float));
+  s->key_cache = (float*)calloc((size_t)p->n_layers * p->seq_len * kv_dim, sizeof(float));
+  s->value_cache = (float*)calloc((size_t)p->n_layers * p->seq_len * kv_dim, sizeof(float));
+  s->att = (float*)calloc((size_t)p->n_heads * p->seq_len, sizeof(float));
+  s->logits = (float*)calloc(p->vocab_size, sizeof(float));
+  if (!s->x || !s->xb || !s->xb2 || !s->hb || !s->hb2 || !s->q || !s->key_cache || !s->value_cache || !s->att ||
+      !s->logits) {
+    fprintf(stderr, "malloc failed!\n");
+    exit(EXIT_FAILURE);
+  }
+}
+
+extern "C" void free_run_state(RunState* s) {
+  free(s->x);
+  free(s->xb);
+  free(s->xb2);
+  free(s->hb);
+  free(s->hb2);
+  free(s->q);
+  free(s->att);
+  free(s->logits);
+  free(s->key_cache);
+  free(s->value_cache);
+}
+
+// reference src/utils.cpp:150-170
+extern "C" void read_checkpoint(char* checkpoint, Config* config, TransformerWeights* weights, int* fd, float** data,
+                                ssize_t* file_size) {
+  FILE* file = fopen(checkpoint, "rb");
+  if (!file) {
+    fprintf(stderr, "Couldn't open file %s\n", checkpoint);
+    exit(EXIT_FAILURE);
+  }
+  if (fread(config, sizeof(Config), 1, file) != 1) exit(EXIT_FAILURE);
+  const int shared_weights = config->vocab_size > 0 ? 1 : 0;
+  config->vocab_size = abs(config->vocab_size);
+  fseek(file, 0, SEEK_END);
+  *file_size = ftell(file);
+  fclose(file);
+  *fd = open(checkpoint, O_RDONLY);
+  if (*fd == -1) {
+    fprintf(stderr, "open failed!\n");
+    exit(EXIT_FAILURE);
+  }
+  *data = (float*)mmap(NULL, *file_size, PROT_READ, MAP_PRIVATE, *fd, 0);
+  if (*data == MAP_FAILED) {
+    fprintf(stderr, "mmap failed!\n");
+    exit(EXIT_FAILURE);
+  }
+  float* weights_ptr = *data + sizeof(Config) / sizeof(float);
+  thallama_map_weights(weights, config, weights_ptr, shared_weights);
+}
+
+// reference src/utils.cpp:106-117
+extern "C" void print_transformer(Transformer* t) {
+  printf("---------Model Information----------\n");
+  printf("dim: %d\n", t->config.dim);
+  printf("hidden_dim: %d\n", t->config.hidden_dim);
+  printf("n_layers: %d\n", t->config.n_layers);
+  printf("n_heads: %d\n", t->config.n_heads);
+  printf("n_kv_heads: %d\n", t->config.n_kv_heads);
+  printf("vocab_size: %d\n", t->config.vocab_size);
+  printf("seq_len: %d\n", t->config.seq_len);
+  printf("weights_size: %lu MB\n", (unsigned long)((t->file_size - sizeof(Config)) / (1024L * 1024L)));
+  printf("------------------------------------\n");
+}
+
+extern "C" void build_transformer(Transformer* t, char* checkpoint_path) {
+  read_checkpoint(checkpoint_path, &t->config, &t->weights, &t->fd, &t->data, &t->file_size);
+  malloc_run_state(&t->state, &t->config);
+  print_transformer(t);
+}
+
+extern "C" void free_transformer(Transformer* t) {
+  if (t->data != MAP_FAILED && t->data) munmap(t->data, t->file_size);
+  if (t->fd != -1) close(t->fd);
+  free_run_state(&t->state);
+}
+
+// ------------------------------------------------------------------ device residency
+extern "C" void copy_weight_to_device(Transformer* t_h, TransformerWeights** w_d) {
+  const Config* p = &t_h->config;
+  const int shared = t_h->weights.wcls == t_h->weights.token_embedding_table;
+  const size_t n = thallama_v0_payload_floats(p, shared);
+  float* arena = nullptr;
+  CHECK_HIP(hipMalloc(&arena, n * sizeof(float)));
+  CHECK_HIP(hipMemcpy(arena, t_h->weights.token_embedding_table, n * sizeof(float), hipMemcpyHostToDevice));
+  *w_d = (TransformerWeights*)malloc(sizeof(TransformerWeights));
+  thallama_map_weights(*w_d, p, arena, shared);
+}
+
+extern "C" void free_weight_device(TransformerWeights* w_d) {
+  if (!w_d) return;
+  CHECK_HIP(hipFree(w_d->token_embedding_table));
+  free(w_d);
+}
+
+// reference src/models.cpp:155-179 (same buffers and shapes, 64-bit sizes)
+extern "C" void alloc_state_to_device_batch(Transformer* t_h, RunState** s_d_batch, int batch_size) {
+  const Config* p = &t_h->config;
+  const size_t dim = p->dim, V = p->vocab_size, L = p->n_layers, H = p->n_heads, S = p->seq_len;
+  const size_t hid = p->hidden_dim, kvd = (size_t)p->dim * p->n_kv_heads / p->n_heads, B = batch_size;
+  RunState* s = (RunState*)calloc(1, sizeof(RunState));
+  CHECK_HIP(hipMalloc(&s->x, dim * B * 4));
+  CHECK_HIP(hipMalloc(&s->xb, dim * B * 4));
+  CHECK_HIP(hipMalloc(&s->xb2, dim * B * 4));
+  CHECK_HIP(hipMalloc(&s->hb, hid * B * 4));
+  CHECK_HIP(hipMalloc(&s->hb2, hid * B * 4));
+  CHECK_HIP(hipMalloc(&s->q, dim * B * 4));
+  CHECK_HIP(hipMalloc(&s->att, H * S * B * 4));
+  CHECK_HIP(hipMalloc(&s->logits, V * B * 4));
+  CHECK_HIP(hipMalloc(&s->key_cache, L * S * kvd * B * 4));
+  CHECK_HIP(hipMalloc(&s->value_cache, L * S * kvd * B * 4));
+  CHECK_HIP(hipMemset(s->key_cache, 0, L * S * kvd * B * 4));
+  CHECK_HIP(hipMemset(s->value_cache, 0, L * S * kvd * B * 4));
+  *s_d_batch = s;
+}
+
+extern "C" void free_state_device(RunState* s) {
+  if (!s) return;
+  float* bufs[] = {s->x, s->xb, s->xb2, s->hb, s->hb2, s->q, s->att, s->logits, s->key_cache, s->value_cache};
+  for (float* b : bufs)
+    if (b) CHECK_HIP(hipFree(b));
+  free(s);
+}
+
+// ------------------------------------------------------------------ synthetic weights
+__global__ void __launch_bounds__(256) k_synth(float* dst, size_t n, uint64_t tseed, float scale) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    dst[i] = tl_synth_value(tseed, i, scale);
+}
+
+__global__ void __launch_bounds__(256) k_fill(float* dst, size_t n, float v) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) dst[i] = v;
+}
+
+extern "C" int thallama_synth_arena(float* arena, const Config* cfg, int shared_weights, uint64_t seed,
+                                    hipStream_t stream) {
+  TlSynthPlan plan;
+  tl_synth_plan(&plan, cfg, shared_weights);
+  for (int t = 0; t < plan.n; ++t) {
+    const TlSynthTensor& e = plan.t[t];
+    if (!e.count) continue;
+    float* dst = arena + e.offset;
+    int blocks = (int)((e.count + 255) / 256);
+    if (blocks > 8192) blocks = 8192;
+    if (e.kind == TL_SYNTH_NORMAL) {
+      hipLaunchKernelGGL(k_synth, dim3(blocks), dim3(256), 0, stream, dst, e.count, tl_synth_tensor_seed(seed, e.id),
+                         tl_synth_scale(e.stddev));
+    } else {
+      hipLaunchKernelGGL(k_fill, dim3(blocks), dim3(256), 0, stream, dst, e.count, e.value);
+    }
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return (int)err;
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------ helpers
+extern "C" int thallama_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+extern "C" int thallama_set_device(int dev) { return (int)hipSetDevice(dev); }
+extern "C" void* thallama_malloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) return nullptr;
+  return p;
+}
+extern "C" int thallama_free(void* p) { return (int)hipFree(p); }
+extern "C" int thallama_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+  return (int)hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice);
+}
+extern "C" int thallama_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+  return (int)hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+}
+extern "C" int thallama_memcpy_d2d(void* dst, const void* src, size_t bytes) {
+  return (int)hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice);
+}
+extern "C" int thallama_memset(void* dst, int value, size_t bytes) { return (int)hipMemset(dst, value, bytes); }
+extern "C" int thallama_sync(void) { return (int)hipDeviceSynchronize(); }

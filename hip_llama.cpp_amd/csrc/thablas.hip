@@ -1,0 +1,211 @@
+// thablas.hip — thaBLAS entry points (include/thaBLAS.hpp) on gfx950.
+//
+// Reference: /root/reference/src/thaBLAS.cpp.  Every GEMV-shaped entry point
+// routes into the one streaming kernel of gemv.hpp; the GEMM-shaped ones
+// (thaBLAS_s_matmul, the N >= 16 case of thaBLAS_s_matmul_reduction,
+// thaBLAS_s_sgemm_Mx16xK) run on the exact-f32 matrix cores
+// (v_mfma_f32_32x32x2_f32), which the reference only sketched
+// (src/thaBLAS.cpp:321-351, behind an undefined MATRIX_CORE switch).
+#include "../../include/thaBLAS.hpp"
+#include "../../include/hip_helper.hpp"
+#include "common.hpp"
+#include "gemv_dispatch.hpp"
+
+using tl::f4;
+
+// ------------------------------------------------------------------ handle
+extern "C" thablasStatus_t thablasCreate(thablasHandle_t* handle) {
+  if (!handle) return THABLAS_STATUS_HANDLE_IS_NULLPTR;
+  int dev = 0;
+  CHECK_HIP(hipGetDevice(&dev));
+  handle->current_gpu_id = dev;
+  CHECK_HIP(hipStreamCreateWithFlags(&handle->calc_stream, hipStreamNonBlocking));
+  CHECK_HIP(hipStreamCreateWithFlags(&handle->copy_stream, hipStreamNonBlocking));
+  return THABLAS_STATUS_SUCCESS;
+}
+
+extern "C" thablasStatus_t thablasDestroy(thablasHandle_t handle) {
+  if (handle.calc_stream) CHECK_HIP(hipStreamDestroy(handle.calc_stream));
+  if (handle.copy_stream) CHECK_HIP(hipStreamDestroy(handle.copy_stream));
+  return THABLAS_STATUS_SUCCESS;
+}
+
+static inline thablasStatus_t launch_status(hipError_t e) {
+  return e == hipSuccess ? THABLAS_STATUS_SUCCESS : THABLAS_STATUS_EXECUTION_FAILED;
+}
+
+// ------------------------------------------------------------------ level 1
+__global__ void __launch_bounds__(256) k_scale_div(int n, const float* A, float* B, float val) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+    B[i] = A[i] / val;  // reference src/thaBLAS.cpp:76 (true division, not x * (1/val))
+}
+
+extern "C" thablasStatus_t thablas_Svds(thablasHandle_t handle, int n, float* A, float* B, float val) {
+  // reference src/thaBLAS.cpp:79-84 rejects these (with a status of ALLOC_FAILED)
+  if (n <= 0 || !A || !B || val == 0.f || handle.current_gpu_id < 0) return THABLAS_STATUS_INVALID_VALUE;
+  int blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(k_scale_div, dim3(blocks), dim3(256), 0, handle.calc_stream, n, A, B, val);
+  return launch_status(hipGetLastError());
+}
+
+__global__ void __launch_bounds__(256) k_vecadd(float* __restrict__ a, const float* __restrict__ b, int n) {
+  const int n4 = n >> 2;
+  f4* a4 = reinterpret_cast<f4*>(a);
+  const f4* b4 = reinterpret_cast<const f4*>(b);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) {
+    f4 x = a4[i], y = b4[i];
+    a4[i] = f4{x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w};
+  }
+  for (int i = (n4 << 2) + blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) a[i] += b[i];
+}
+
+__global__ void __launch_bounds__(256) k_vecadd_scalar(float* a, const float* b, int n) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) a[i] += b[i];
+}
+
+extern "C" thablasStatus_t thaBLAS_s_vecaddvec(thablasHandle_t* handle, float* a, float* b, int size) {
+  if (!handle) return THABLAS_STATUS_HANDLE_IS_NULLPTR;
+  if (size < 0 || ((!a || !b) && size)) return THABLAS_STATUS_INVALID_VALUE;
+  if (size == 0) return THABLAS_STATUS_SUCCESS;
+  int blocks = (size / 4 + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
+  if ((((uintptr_t)a | (uintptr_t)b) & 15) == 0)
+    hipLaunchKernelGGL(k_vecadd, dim3(blocks), dim3(256), 0, handle->calc_stream, a, b, size);
+  else
+    hipLaunchKernelGGL(k_vecadd_scalar, dim3(blocks), dim3(256), 0, handle->calc_stream, a, b, size);
+  return launch_status(hipGetLastError());
+}
+
+// ------------------------------------------------------------------ level 2
+static thablasStatus_t gemv_store(hipStream_t s, int nb, float* C, float* B, float* A, int K, int M,
+                                  long long Coff, int has_pos, const int* pos_d, long long Cbs,
+                                  long long Bbs) {
+  if (nb < 0 || K < 0 || M < 0) return THABLAS_STATUS_INVALID_VALUE;
+  if (nb == 0 || M == 0) return THABLAS_STATUS_SUCCESS;
+  if (!C || !A || (!B && K) || (has_pos && !pos_d)) return THABLAS_STATUS_INVALID_VALUE;
+  tl::GemvParams p = {};
+  p.W0 = A;
+  p.K = K;
+  p.n_items = M;
+  p.nb = nb;
+  p.x = B;
+  p.x_stride = Bbs;
+  p.y = C;
+  p.y_stride = Cbs;
+  p.y_off = Coff;
+  p.has_pos = has_pos;
+  p.pos = pos_d;
+  if (K == 0) {  // empty reduction: C = 0 (handled by the generic path with no loads)
+    hipLaunchKernelGGL((tl::gemv_generic_kernel<tl::GM_STORE>), dim3((M + 3) / 4, nb), dim3(256), 0, s, p);
+    return launch_status(hipGetLastError());
+  }
+  return launch_status(tl::launch_gemv(tl::GM_STORE, p, s, false));
+}
+
+extern "C" thablasStatus_t thaBLAS_s_matmul_batch(thablasHandle_t* handle, int n_batches,
+                                                  float* C_batch, float* B_batch, float* A, int K,
+                                                  int M, int Coff, int has_pos, int pos_d[],
+                                                  int C_batch_size, int B_batch_size) {
+  if (!handle) return THABLAS_STATUS_HANDLE_IS_NULLPTR;
+  return gemv_store(handle->calc_stream, n_batches, C_batch, B_batch, A, K, M, Coff, has_pos, pos_d,
+                    C_batch_size, B_batch_size);
+}
+
+extern "C" thablasStatus_t thaBLAS_s_matmulvec(thablasHandle_t handle, float* C, float* B, float* A, int K, int M) {
+  return gemv_store(handle.calc_stream, 1, C, B, A, K, M, 0, 0, nullptr, M, K);
+}
+
+extern "C" thablasStatus_t thaDNN_s_matmulvec_v2(thablasHandle_t handle, float* C, float* B, float* A, int K, int M) {
+  return gemv_store(handle.calc_stream, 1, C, B, A, K, M, 0, 0, nullptr, M, K);
+}
+
+// ------------------------------------------------------------------ level 3 (MFMA f32)
+// C[i][j] = sum_k A(i,k) * B(k,j) with generic strides (elements):
+//   A(i,k) = A[i*sai + k*sak], B(k,j) = B[k*sbk + j*sbj], C[i*sci + j*scj].
+// 64x64 block tile, 4 waves in 2x2, each wave one 32x32 v_mfma_f32_32x32x2_f32
+// accumulator; K staged through LDS 16 at a time.  Exact f32: each output is a
+// k-ordered fmaf chain (cdna_hip_programming.md §3 FP32-input MFMA).
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+__global__ void __launch_bounds__(256) k_sgemm_mfma(int M, int N, int K, const float* __restrict__ A,
+                                                    long long sai, long long sak,
+                                                    const float* __restrict__ B, long long sbk,
+                                                    long long sbj, float* __restrict__ C,
+                                                    long long sci, long long scj) {
+  constexpr int BM = 64, BN = 64, BK = 16;
+  __shared__ float As[BK][BM + 1];
+  __shared__ float Bs[BK][BN + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int i0 = blockIdx.y * BM, j0 = blockIdx.x * BN;
+  f16v acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int k0 = 0; k0 < K; k0 += BK) {
+    for (int e = tid; e < BK * BM; e += 256) {
+      const int kk = e / BM, ii = e % BM;
+      const int gi = i0 + ii, gk = k0 + kk;
+      As[kk][ii] = (gi < M && gk < K) ? A[gi * sai + gk * sak] : 0.f;
+    }
+    for (int e = tid; e < BK * BN; e += 256) {
+      const int kk = e / BN, jj = e % BN;
+      const int gj = j0 + jj, gk = k0 + kk;
+      Bs[kk][jj] = (gj < N && gk < K) ? B[gk * sbk + gj * sbj] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2) {
+      const float a = As[kk + (lane >> 5)][wm * 32 + (lane & 31)];
+      const float b = Bs[kk + (lane >> 5)][wn * 32 + (lane & 31)];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  const int col = j0 + wn * 32 + (lane & 31);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = i0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (row < M && col < N) C[row * sci + col * scj] = acc[r];
+  }
+}
+
+static thablasStatus_t sgemm(hipStream_t s, int M, int N, int K, const float* A, long long sai,
+                             long long sak, const float* B, long long sbk, long long sbj, float* C,
+                             long long sci, long long scj) {
+  if (M <= 0 || N <= 0) return THABLAS_STATUS_SUCCESS;
+  dim3 grid((N + 63) / 64, (M + 63) / 64);
+  hipLaunchKernelGGL(k_sgemm_mfma, grid, dim3(256), 0, s, M, N, K, A, sai, sak, B, sbk, sbj, C, sci, scj);
+  return launch_status(hipGetLastError());
+}
+
+extern "C" thablasStatus_t thaBLAS_s_matmul(thablasHandle_t handle, int m, int n, int k, float* A, float* B, float* C) {
+  // reference src/thaBLAS.cpp:157-160: all three sizes must be non-zero
+  if (m <= 0 || n <= 0 || k <= 0 || !A || !B || !C || handle.current_gpu_id < 0)
+    return THABLAS_STATUS_INVALID_VALUE;
+  return sgemm(handle.calc_stream, m, n, k, A, k, 1, B, n, 1, C, n, 1);
+}
+
+extern "C" thablasStatus_t thaBLAS_s_matmul_reduction(thablasHandle_t* handle, float* A, float* B, float* C,
+                                                      int M, int N, int K) {
+  if (!handle) return THABLAS_STATUS_HANDLE_IS_NULLPTR;
+  if (M < 0 || N < 0 || K < 0 || !A || !B || !C) return THABLAS_STATUS_INVALID_VALUE;
+  // C[j][i] = sum_k A[i][k] B[j][k]: N independent GEMVs that share A.  Up to 16
+  // columns the streaming GEMV reads A once for all of them; beyond that the
+  // problem is GEMM-shaped and goes to the matrix cores.
+  if (N <= 16) return gemv_store(handle->calc_stream, N, C, B, A, K, M, 0, 0, nullptr, M, K);
+  return sgemm(handle->calc_stream, M, N, K, A, K, 1, B, 1, K, C, 1, M);
+}
+
+extern "C" thablasStatus_t thaBLAS_s_sgemm_Mx16xK(thablasHandle_t* handle, float* d_A, float* d_B, float* d_D,
+                                                  int M, int N, int K) {
+  if (!handle) return THABLAS_STATUS_HANDLE_IS_NULLPTR;
+  if (M < 0 || N < 0 || K < 0 || !d_A || !d_B || !d_D) return THABLAS_STATUS_INVALID_VALUE;
+  // D[n][m] = sum_k A[m][k] B[n][k] (reference kernel: B and D column-major, N = 16)
+  return sgemm(handle->calc_stream, M, N, K, d_A, K, 1, d_B, 1, K, d_D, 1, M);
+}
+
+extern "C" thablasStatus_t thaBLAS_s_matmul_ifdef(thablasHandle_t* handle, float* d_A, float* d_B, float* d_D,
+                                                  int M, int N, int K) {
+  return thaBLAS_s_matmul_reduction(handle, d_A, d_B, d_D, M, N, K);
+}

@@ -1,0 +1,348 @@
+"""ctypes bindings of libthallama.so (include/thaBLAS.hpp, include/thaDNN.hpp,
+include/models.hpp, include/thallama.h).
+
+Host-side mirror of the reference's operator interface: the same entry-point
+names, argument meaning and status codes as /root/reference/include/thaBLAS.hpp
+and thaDNN.hpp, so tests read like the reference's own GPU-vs-CPU tests
+(scripts/test/thaDNN.test.cpp).  There is deliberately NO fallback: if the HIP
+library is missing or no GPU is present, calls raise.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import LIB_PATH
+
+# ---------------------------------------------------------------- ABI types
+c_float_p = C.POINTER(C.c_float)
+c_int_p = C.POINTER(C.c_int)
+
+
+class Config(C.Structure):
+    """reference include/models.hpp:10-18"""
+    _fields_ = [("dim", C.c_int), ("hidden_dim", C.c_int), ("n_layers", C.c_int), ("n_heads", C.c_int),
+                ("n_kv_heads", C.c_int), ("vocab_size", C.c_int), ("seq_len", C.c_int)]
+
+    @classmethod
+    def make(cls, dim, hidden_dim, n_layers, n_heads, n_kv_heads, vocab_size, seq_len):
+        return cls(dim, hidden_dim, n_layers, n_heads, n_kv_heads, vocab_size, seq_len)
+
+    def as_tuple(self):
+        return tuple(getattr(self, f) for f, _ in self._fields_)
+
+    @property
+    def head_size(self):
+        return self.dim // self.n_heads
+
+    @property
+    def kv_dim(self):
+        return self.dim * self.n_kv_heads // self.n_heads
+
+
+class TransformerWeights(C.Structure):
+    """reference include/models.hpp:20-39"""
+    _fields_ = [(n, c_float_p) for n in ("token_embedding_table", "rms_att_weight", "rms_ffn_weight", "wq", "wk",
+                                          "wv", "wo", "w1", "w2", "w3", "rms_final_weight", "wcls")]
+
+
+class RunState(C.Structure):
+    """reference include/models.hpp:41-60"""
+    _fields_ = [(n, c_float_p) for n in ("x", "xb", "xb2", "hb", "hb2", "q", "k", "v", "att", "logits", "key_cache",
+                                          "value_cache", "key_matmul", "value_matmul", "key_layer_cache",
+                                          "value_layer_cache")]
+
+
+class Transformer(C.Structure):
+    """reference include/models.hpp:62-70"""
+    _fields_ = [("config", Config), ("weights", TransformerWeights), ("state", RunState), ("fd", C.c_int),
+                ("data", c_float_p), ("file_size", C.c_ssize_t)]
+
+
+class Handle(C.Structure):
+    """thablasHandle_t, reference include/thaBLAS.hpp:21-25"""
+    _fields_ = [("current_gpu_id", C.c_int), ("calc_stream", C.c_void_p), ("copy_stream", C.c_void_p)]
+
+
+STATUS = {0: "SUCCESS", 1: "NOT_INITIALIZED", 2: "ALLOC_FAILED", 3: "INVALID_VALUE", 4: "MAPPING_ERROR",
+          5: "EXECUTION_FAILED", 6: "INTERNAL_ERROR", 7: "NOT_SUPPORTED", 8: "ARCH_MISMATCH",
+          9: "HANDLE_IS_NULLPTR", 10: "INVALID_ENUM", 11: "UNKNOWN"}
+
+# kernel classes (include/thallama.h)
+K_QKV, K_ATTN, K_WO, K_FFN_UP, K_FFN_DOWN, K_CLS, K_ARGMAX = range(7)
+K_NAMES = ["qkv", "attn", "wo", "ffn_up", "ffn_down", "cls", "argmax"]
+OPT_NT_WEIGHTS, OPT_ATTN_SPLITS, OPT_USE_GRAPH, OPT_PROFILE = 1, 2, 3, 4
+
+_lib = None
+
+
+def lib():
+    """Load libthallama.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        P, I, F, VP, S = c_float_p, C.c_int, C.c_float, C.c_void_p, C.c_size_t
+        sig = {
+            "thablasCreate": (I, [C.POINTER(Handle)]),
+            "thablasDestroy": (I, [Handle]),
+            "thablas_Svds": (I, [Handle, I, P, P, F]),
+            "thaBLAS_s_vecaddvec": (I, [C.POINTER(Handle), P, P, I]),
+            "thaBLAS_s_matmulvec": (I, [Handle, P, P, P, I, I]),
+            "thaDNN_s_matmulvec_v2": (I, [Handle, P, P, P, I, I]),
+            "thaBLAS_s_matmul": (I, [Handle, I, I, I, P, P, P]),
+            "thaBLAS_s_matmul_batch": (I, [C.POINTER(Handle), I, P, P, P, I, I, I, I, c_int_p, I, I]),
+            "thaBLAS_s_matmul_reduction": (I, [C.POINTER(Handle), P, P, P, I, I, I]),
+            "thaBLAS_s_sgemm_Mx16xK": (I, [C.POINTER(Handle), P, P, P, I, I, I]),
+            "thaBLAS_s_matmul_ifdef": (I, [C.POINTER(Handle), P, P, P, I, I, I]),
+            "thaDNN_s_rmsnorm_v2_batch": (I, [C.POINTER(Handle), I, P, P, P, I, I]),
+            "thaDNN_s_rope": (I, [C.POINTER(Handle), I, I, I, I, P, P]),
+            "thaDNN_s_swiglu": (I, [C.POINTER(Handle), P, P, I]),
+            "thaDNN_s_softmax_v2": (I, [C.POINTER(Handle), P, I]),
+            "thaDNN_s_multiheads_1_v1_batch": (I, [C.POINTER(Handle), I, c_int_p, c_int_p, I, I, P, P, P, I, I, I, I,
+                                                   I, I]),
+            "thaDNN_s_multiheads_2_v1_batch": (I, [C.POINTER(Handle), I, P, c_int_p, I, I]),
+            "thaDNN_s_multiheads_3_v1_batch": (I, [C.POINTER(Handle), I, c_int_p, I, P, P, P, I, I, I, I, I, I, I]),
+            "thaDNN_s_multiheads_1_v2_batch": (I, [C.POINTER(Handle), I, I, c_int_p, c_int_p, I, P, P, P, I, I, I, I,
+                                                   I]),
+            "thaDNN_s_multiheads_2_batch": (I, [C.POINTER(Handle), I, P, c_int_p, I, I]),
+            "thaDNN_s_multiheads_3_v2_batch": (I, [C.POINTER(Handle), I, c_int_p, I, P, P, P, I, I, I, I, I, I]),
+            "thaDNN_s_forward_batch": (I, [Handle, Handle, Handle, I, C.POINTER(Config), C.POINTER(TransformerWeights),
+                                           C.POINTER(RunState), c_int_p, c_int_p, P]),
+            "thallama_v0_payload_floats": (S, [C.POINTER(Config), I]),
+            "thallama_map_weights": (None, [C.POINTER(TransformerWeights), C.POINTER(Config), P, I]),
+            "alloc_state_to_device_batch": (None, [C.POINTER(Transformer), C.POINTER(C.POINTER(RunState)), I]),
+            "free_state_device": (None, [C.POINTER(RunState)]),
+            "thallama_decoder_create": (I, [C.POINTER(VP), C.POINTER(Config), C.POINTER(TransformerWeights),
+                                            C.POINTER(RunState), I, VP]),
+            "thallama_decoder_destroy": (None, [VP]),
+            "thallama_decoder_set": (I, [VP, I, I]),
+            "thallama_decoder_stream": (VP, [VP]),
+            "thallama_decoder_forward": (I, [VP, c_int_p, c_int_p, P]),
+            "thallama_decoder_greedy": (I, [VP, c_int_p, c_int_p, I, c_int_p, I]),
+            "thallama_decoder_logits": (I, [VP, P]),
+            "thallama_decoder_prof": (I, [VP, I, C.POINTER(C.c_double), C.POINTER(C.c_longlong)]),
+            "thallama_decoder_prof_reset": (None, [VP]),
+            "thallama_step_bytes": (C.c_double, [C.POINTER(Config), I, I, c_int_p]),
+            "thallama_synth_arena": (I, [P, C.POINTER(Config), I, C.c_uint64, VP]),
+            "thallama_device_count": (I, []),
+            "thallama_set_device": (I, [I]),
+            "thallama_malloc": (VP, [S]),
+            "thallama_free": (I, [VP]),
+            "thallama_memcpy_h2d": (I, [VP, VP, S]),
+            "thallama_memcpy_d2h": (I, [VP, VP, S]),
+            "thallama_memcpy_d2d": (I, [VP, VP, S]),
+            "thallama_memset": (I, [VP, I, S]),
+            "thallama_sync": (I, []),
+            "thallama_last_error": (C.c_char_p, []),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, what="call"):
+    if rc != 0:
+        err = lib().thallama_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed with status {rc} ({STATUS.get(rc, rc)}) {err}")
+    return rc
+
+
+def device_count():
+    return lib().thallama_device_count()
+
+
+# ---------------------------------------------------------------- device memory
+class DevBuf:
+    """Owning device allocation (hipMalloc) with numpy transfer helpers."""
+
+    def __init__(self, nbytes):
+        self.nbytes = int(nbytes)
+        self.ptr = lib().thallama_malloc(self.nbytes)
+        if not self.ptr:
+            raise MemoryError(f"hipMalloc({self.nbytes}) failed")
+
+    @classmethod
+    def from_array(cls, a):
+        a = np.ascontiguousarray(a)
+        b = cls(a.nbytes)
+        b.upload(a)
+        return b
+
+    def upload(self, a, offset=0):
+        a = np.ascontiguousarray(a)
+        check(lib().thallama_memcpy_h2d(C.c_void_p(self.ptr + offset), a.ctypes.data_as(C.c_void_p), a.nbytes), "h2d")
+
+    def download(self, dtype=np.float32, count=None, offset=0):
+        dtype = np.dtype(dtype)
+        n = (self.nbytes - offset) // dtype.itemsize if count is None else count
+        out = np.empty(n, dtype=dtype)
+        check(lib().thallama_memcpy_d2h(out.ctypes.data_as(C.c_void_p), C.c_void_p(self.ptr + offset),
+                                        out.nbytes), "d2h")
+        return out
+
+    def fptr(self, offset_elems=0):
+        return C.cast(C.c_void_p(self.ptr + 4 * offset_elems), c_float_p)
+
+    def iptr(self, offset_elems=0):
+        return C.cast(C.c_void_p(self.ptr + 4 * offset_elems), c_int_p)
+
+    def free(self):
+        if self.ptr:
+            lib().thallama_free(C.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def new_handle():
+    h = Handle()
+    rc = lib().thablasCreate(C.byref(h))
+    if rc != 0:
+        raise RuntimeError(f"thablasCreate: {STATUS.get(rc, rc)}")
+    return h
+
+
+def sync():
+    check(lib().thallama_sync(), "hipDeviceSynchronize")
+
+
+# ---------------------------------------------------------------- model / state
+class DeviceModel:
+    """Weights in ONE device arena with the v0 payload layout (reference src/utils.cpp:119-148).
+
+    Either filled by the deterministic synthetic generator on the device
+    (``seed``), or uploaded from a host v0 payload (``payload``, e.g. a model.bin
+    minus its 28-byte header, or the oracle's arena)."""
+
+    def __init__(self, cfg, shared, seed=None, payload=None, arena_ptr=None):
+        self.cfg = cfg
+        self.shared = int(bool(shared))
+        self.n = lib().thallama_v0_payload_floats(C.byref(cfg), self.shared)
+        self.buf = None
+        if arena_ptr is None:
+            self.buf = DevBuf(self.n * 4)
+            base = self.buf.ptr
+        else:
+            base = arena_ptr  # caller-owned (e.g. a torch tensor's data_ptr)
+        self.base = base
+        if payload is not None:
+            payload = np.ascontiguousarray(payload, dtype=np.float32)
+            assert payload.size == self.n, (payload.size, self.n)
+            check(lib().thallama_memcpy_h2d(C.c_void_p(base), payload.ctypes.data_as(C.c_void_p), payload.nbytes))
+        elif seed is not None:
+            check(lib().thallama_synth_arena(C.cast(C.c_void_p(base), c_float_p), C.byref(cfg), self.shared,
+                                             C.c_uint64(seed), None), "synth")
+            sync()
+        self.w = TransformerWeights()
+        lib().thallama_map_weights(C.byref(self.w), C.byref(cfg), C.cast(C.c_void_p(base), c_float_p), self.shared)
+
+    def arena_ptr(self):
+        return self.base
+
+    def download(self):
+        out = np.empty(self.n, dtype=np.float32)
+        check(lib().thallama_memcpy_d2h(out.ctypes.data_as(C.c_void_p), C.c_void_p(self.base), out.nbytes))
+        return out
+
+
+class DeviceState:
+    """Batched RunState (reference src/models.cpp:155-179)."""
+
+    def __init__(self, cfg, batch):
+        self.cfg = cfg
+        self.batch = batch
+        t = Transformer()
+        t.config = cfg
+        p = C.POINTER(RunState)()
+        lib().alloc_state_to_device_batch(C.byref(t), C.byref(p), batch)
+        self.ptr = p
+        self.s = p.contents
+
+    def free(self):
+        if self.ptr:
+            lib().free_state_device(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Decoder:
+    """The fused decode step (thaDNN_s_forward_batch) as an object (include/thallama.h)."""
+
+    def __init__(self, model, state, batch=None, stream=None):
+        self.model, self.state = model, state
+        self.cfg = model.cfg
+        self.batch = batch or state.batch
+        h = C.c_void_p()
+        check(lib().thallama_decoder_create(C.byref(h), C.byref(self.cfg), C.byref(model.w), C.byref(state.s),
+                                            self.batch, stream), "decoder_create")
+        self.h = h
+
+    @property
+    def vocab(self):
+        return abs(self.cfg.vocab_size)
+
+    def set(self, key, value):
+        check(lib().thallama_decoder_set(self.h, key, int(value)), "decoder_set")
+
+    def forward(self, tokens, pos, want_logits=True):
+        tok = (C.c_int * self.batch)(*[int(t) for t in tokens])
+        ps = (C.c_int * self.batch)(*[int(p) for p in pos])
+        out = np.empty(self.batch * self.vocab, dtype=np.float32) if want_logits else None
+        check(lib().thallama_decoder_forward(self.h, tok, ps, out.ctypes.data_as(c_float_p) if want_logits else None),
+              "decoder_forward")
+        return out.reshape(self.batch, self.vocab) if want_logits else None
+
+    def greedy(self, tokens0, pos0, n_steps, want_tokens=True, sync=True):
+        tok = (C.c_int * self.batch)(*[int(t) for t in tokens0])
+        ps = (C.c_int * self.batch)(*[int(p) for p in pos0])
+        out = (C.c_int * (n_steps * self.batch))() if want_tokens else None
+        check(lib().thallama_decoder_greedy(self.h, tok, ps, n_steps, out, int(sync)), "decoder_greedy")
+        if want_tokens:
+            return np.frombuffer(out, dtype=np.int32).reshape(n_steps, self.batch).copy()
+        return None
+
+    def logits(self):
+        out = np.empty(self.batch * self.vocab, dtype=np.float32)
+        check(lib().thallama_decoder_logits(self.h, out.ctypes.data_as(c_float_p)), "decoder_logits")
+        return out.reshape(self.batch, self.vocab)
+
+    def prof(self, kclass):
+        ms, n = C.c_double(), C.c_longlong()
+        check(lib().thallama_decoder_prof(self.h, kclass, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def prof_reset(self):
+        lib().thallama_decoder_prof_reset(self.h)
+
+    def stream(self):
+        return lib().thallama_decoder_stream(self.h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().thallama_decoder_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def step_bytes(cfg, batch, kclass, pos):
+    arr = (C.c_int * batch)(*[int(p) for p in pos])
+    return lib().thallama_step_bytes(C.byref(cfg), batch, kclass, arr)

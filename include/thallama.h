@@ -1,0 +1,96 @@
+/* thallama.h — native runtime entry points of the MI355X build that sit beside the
+ * reference-compatible thaBLAS/thaDNN surface.  Plain C ABI: opaque handles,
+ * plain pointers and sizes; bound from C++ (apps/), ctypes (tests/, bench.py).
+ *
+ *  - decoder: the fused decode step of thaDNN_s_forward_batch
+ *    (reference src/thaDNN.cpp:13-81) as a reusable object that owns its
+ *    workspace (device token/pos, RoPE table, attention partials), can keep the
+ *    whole greedy loop on the device (argmax feeding the next token; reference
+ *    samples on the host every step, src/llama.cpp:1027-1050) and can replay
+ *    one step as a hipGraph.
+ *  - synthetic weights: deterministic counter-based N(0, sigma)-shaped init
+ *    (train/model.py:232-247 distribution), bit-identical to the host oracle's
+ *    generator (oracle/oracle.c).
+ *  - small device-memory helpers so tests need nothing but ctypes.
+ */
+#ifndef THALLAMA_H
+#define THALLAMA_H
+#include <stddef.h>
+#include <stdint.h>
+#include "models.hpp"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct thallama_decoder thallama_decoder;
+
+/* Option keys for thallama_decoder_set */
+enum {
+  THALLAMA_OPT_NT_WEIGHTS = 1,   /* 0/1: non-temporal weight loads (default: 1 if weights > 1 GiB) */
+  THALLAMA_OPT_ATTN_SPLITS = 2,  /* key splits per (head, seq); 0 = auto */
+  THALLAMA_OPT_USE_GRAPH = 3,    /* 0/1: replay greedy steps from a captured hipGraph */
+  THALLAMA_OPT_PROFILE = 4,      /* 0/1: HIP events around every kernel class (eager only) */
+};
+
+/* Kernel classes for profiling */
+enum {
+  THALLAMA_K_QKV = 0, THALLAMA_K_ATTN = 1, THALLAMA_K_WO = 2, THALLAMA_K_FFN_UP = 3,
+  THALLAMA_K_FFN_DOWN = 4, THALLAMA_K_CLS = 5, THALLAMA_K_ARGMAX = 6, THALLAMA_K_COUNT = 7
+};
+
+/* w and s hold DEVICE pointers (as produced by copy_weight_to_device /
+ * alloc_state_to_device_batch or any equivalent layout).  stream may be 0:
+ * the decoder then creates its own non-blocking stream.  Returns 0 on success. */
+int thallama_decoder_create(thallama_decoder** out, const Config* cfg, const TransformerWeights* w,
+                            const RunState* s, int batch, hipStream_t stream);
+void thallama_decoder_destroy(thallama_decoder* d);
+int thallama_decoder_set(thallama_decoder* d, int key, int value);
+hipStream_t thallama_decoder_stream(thallama_decoder* d);
+
+/* One synchronous step with host token/pos, logits copied to logits_h[batch*vocab]
+ * (logits_h may be NULL).  Exactly thaDNN_s_forward_batch's contract. */
+int thallama_decoder_forward(thallama_decoder* d, const int* token_h, const int* pos_h, float* logits_h);
+
+/* Greedy decode n_steps on the device.  Sequence b starts from token0_h[b] at
+ * pos0_h[b]; step i writes the argmax token of every sequence to
+ * tokens_out_h[i*batch + b] (may be NULL).  Asynchronous unless sync != 0.
+ * Returns 0 on success. */
+int thallama_decoder_greedy(thallama_decoder* d, const int* token0_h, const int* pos0_h, int n_steps,
+                            int* tokens_out_h, int sync);
+
+/* Copy the device logits of the last step into logits_h[batch*vocab] (synchronous). */
+int thallama_decoder_logits(thallama_decoder* d, float* logits_h);
+
+/* Profiling (THALLAMA_OPT_PROFILE=1): accumulated ms and launch count per kernel class
+ * since the last reset. */
+int thallama_decoder_prof(thallama_decoder* d, int kclass, double* total_ms, long long* count);
+void thallama_decoder_prof_reset(thallama_decoder* d);
+
+/* Algorithmic HBM bytes of one step for kernel class kclass at the given positions
+ * (weights once + KV rows read/written), used for roofline reporting. */
+double thallama_step_bytes(const Config* cfg, int batch, int kclass, const int* pos_h);
+
+/* ---- synthetic weights ------------------------------------------------- */
+/* Fill a v0 arena (layout of thallama_map_weights) with the deterministic synthetic
+ * model: N(0,0.02)-shaped linears/embedding, wo & w3 scaled by 1/sqrt(2L), norms 1,
+ * the unused freq_cis block 0.  `arena` is a DEVICE pointer; enqueued on stream. */
+int thallama_synth_arena(float* arena, const Config* cfg, int shared_weights, uint64_t seed,
+                         hipStream_t stream);
+
+/* ---- device memory helpers (ctypes convenience) ------------------------ */
+int thallama_device_count(void);
+int thallama_set_device(int dev);
+void* thallama_malloc(size_t bytes);
+int thallama_free(void* p);
+int thallama_memcpy_h2d(void* dst, const void* src, size_t bytes);
+int thallama_memcpy_d2h(void* dst, const void* src, size_t bytes);
+int thallama_memcpy_d2d(void* dst, const void* src, size_t bytes);
+int thallama_memset(void* dst, int value, size_t bytes);
+int thallama_sync(void);
+const char* thallama_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,148 @@
+"""GPU parity of the fused decode step against the CPU oracle (a bit-exact restatement of the
+reference's src/seq.cpp forward, pinned in tests/test_oracle.py).
+
+Bar (BASELINE.json north_star): greedy token ids identical, fp32 logits within 1e-4 under the
+reference's abs-or-rel rule (scripts/test/thaDNN.test.cpp:224-229).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from helpers import LLAMA2_7B, SMALL, SMALL_GQA, STORIES_110M, TINY, assert_ref_close
+
+pytestmark = pytest.mark.gpu
+
+
+def build(tl, oracle, cfg, shared, seed, batch=1):
+    """Same synthetic weights on both sides: the GPU fills its arena with the device generator,
+    the oracle with the host generator (bit-identical, checked in test_synth_bitexact)."""
+    c = tl.Config.make(*cfg)
+    model = tl.DeviceModel(c, shared, seed=seed)
+    state = tl.DeviceState(c, batch)
+    dec = tl.Decoder(model, state)
+    ref = oracle.Model(cfg, shared, seed=seed)
+    return c, model, state, dec, ref
+
+
+def test_synth_bitexact(gpu, oracle):
+    cfg = SMALL_GQA
+    c = gpu.Config.make(*cfg)
+    m = gpu.DeviceModel(c, 0, seed=1234)
+    ref = oracle.Model(cfg, 0, seed=1234)
+    np.testing.assert_array_equal(m.download(), ref.arena())
+
+
+@pytest.mark.parametrize("cfg,shared", [(TINY, 0), (SMALL, 0), (SMALL_GQA, 0), (SMALL, 1)])
+@pytest.mark.parametrize("graph", [0, 1])
+def test_greedy_matches_oracle(gpu, oracle, cfg, shared, graph):
+    c, model, state, dec, ref = build(gpu, oracle, cfg, shared, seed=42)
+    dec.set(gpu.OPT_USE_GRAPH, graph)
+    n = 40
+    want = ref.greedy(1, 0, n)
+    got = dec.greedy([1], [0], n)[:, 0].tolist()
+    assert got == want
+    # the device still holds the last step's logits (token want[-2] at pos n-1)
+    fresh = oracle.Model(cfg, shared, seed=42)
+    for p, t in enumerate([1] + want[:-1]):
+        last = fresh.forward(t, p)
+    assert_ref_close(dec.logits()[0], last, 1e-4, "last-step logits")
+
+
+@pytest.mark.parametrize("cfg,shared", [(TINY, 0), (SMALL, 1), (SMALL_GQA, 0)])
+def test_forced_logits_every_step(gpu, oracle, cfg, shared):
+    """Teacher-forced random tokens: every step's logits within 1e-4 (also covers shared
+    classifiers, whose greedy path degenerates to repeating the input token)."""
+    c, model, state, dec, ref = build(gpu, oracle, cfg, shared, seed=9)
+    toks = np.random.default_rng(3).integers(0, cfg[5], 24)
+    for p, t in enumerate(toks):
+        got = dec.forward([int(t)], [p])[0]
+        want = ref.forward(int(t), p)
+        assert_ref_close(got, want, 1e-4, f"logits pos {p}")
+        assert int(np.argmax(got)) == oracle.lib().oracle_argmax(oracle.fp(want), cfg[5])
+
+
+@pytest.mark.parametrize("B", [2, 3, 8])
+def test_batch_independent_positions(gpu, oracle, B):
+    """B sequences at different positions in one step == B independent CPU decodes."""
+    cfg = SMALL_GQA
+    c, model, state, dec, _ = build(gpu, oracle, cfg, 0, seed=5, batch=B)
+    rng = np.random.default_rng(B)
+    starts = rng.integers(0, 20, B)
+    toks = rng.integers(0, cfg[5], (B, 64))
+    refs = [oracle.Model(cfg, 0, seed=5) for _ in range(B)]
+    for b in range(B):
+        for p in range(int(starts[b])):
+            refs[b].forward(int(toks[b, p]), p)
+    # prefix: every lane runs (toks[b,p], p); for p >= starts[b] that row is rewritten by the real
+    # step at p before any attention reads it, so the extra work is harmless
+    for p in range(int(starts.max())):
+        dec.forward([int(toks[b, p]) for b in range(B)], [p] * B, want_logits=False)
+    for step in range(12):
+        ps = [int(starts[b]) + step for b in range(B)]
+        tk = [int(toks[b, ps[b]]) for b in range(B)]
+        got = dec.forward(tk, ps)
+        for b in range(B):
+            assert_ref_close(got[b], refs[b].forward(tk[b], ps[b]), 1e-4, f"b={b} pos={ps[b]}")
+
+
+def test_forward_batch_c_abi(gpu, oracle):
+    """thaDNN_s_forward_batch, called exactly like the reference driver does
+    (src/llama.cpp:1017): host token[]/pos[], logits into a host buffer."""
+    cfg = SMALL
+    c = gpu.Config.make(*cfg)
+    model = gpu.DeviceModel(c, 0, seed=77)
+    B = 2
+    state = gpu.DeviceState(c, B)
+    h = gpu.new_handle()
+    ref = [oracle.Model(cfg, 0, seed=77) for _ in range(B)]
+    logits = np.zeros(B * cfg[5], np.float32)
+    toks = [[1, 5, 9, 200, 7], [3, 3, 100, 44, 2]]
+    for p in range(5):
+        tk = (C.c_int * B)(toks[0][p], toks[1][p])
+        ps = (C.c_int * B)(p, p)
+        rc = gpu.lib().thaDNN_s_forward_batch(h, h, h, B, C.byref(c), C.byref(model.w), state.ptr, tk, ps,
+                                              logits.ctypes.data_as(gpu.c_float_p))
+        assert rc == 0
+        for b in range(B):
+            assert_ref_close(logits[b * cfg[5]:(b + 1) * cfg[5]], ref[b].forward(toks[b][p], p), 1e-4, "abi")
+
+
+@pytest.mark.parametrize("token,pos", [(0, 0), (3, 4), (4, 4), (64, 64)])
+def test_stories110m_reference_cases(gpu, oracle, token, pos):
+    """The reference's own forward test points (scripts/test/thaDNN.test.cpp:541-549) on a
+    stories110M-shaped synthetic model: fresh state, a single forward at (token, pos)."""
+    oracle.set_threads(16)
+    c, model, state, dec, ref = build(gpu, oracle, STORIES_110M, 1, seed=110)
+    got = dec.forward([token], [pos])[0]
+    want = ref.forward(token, pos)
+    assert_ref_close(got, want, 1e-4, "110M logits")
+
+
+def test_stories110m_greedy(gpu, oracle):
+    oracle.set_threads(16)
+    cfg = (768, 2048, 12, 12, 12, 32000, 1024)
+    # unshared classifier so the greedy path does not collapse onto the input token
+    c, model, state, dec, ref = build(gpu, oracle, cfg, 0, seed=111)
+    dec.set(gpu.OPT_USE_GRAPH, 1)
+    n = 48
+    want = ref.greedy(1, 0, n)
+    got = dec.greedy([1], [0], n)[:, 0].tolist()
+    assert got == want
+
+
+@pytest.mark.slow
+def test_llama2_7b_shape(gpu, oracle):
+    """Full llama2-7B shape (26.9 GB fp32): greedy tokens and logits vs the CPU oracle for a
+    few steps (the oracle runs 16 threads; results are thread-count independent)."""
+    oracle.set_threads(16)
+    c, model, state, dec, ref = build(gpu, oracle, LLAMA2_7B, 0, seed=7)
+    dec.set(gpu.OPT_USE_GRAPH, 1)
+    n = 4
+    toks = [1]
+    for p in range(n):
+        want = ref.forward(toks[-1], p)
+        got = dec.forward([toks[-1]], [p])[0]
+        assert_ref_close(got, want, 1e-4, f"7B logits pos {p}")
+        assert int(np.argmax(got)) == int(np.argmax(want))
+        toks.append(int(np.argmax(want)))
