@@ -45,24 +45,33 @@ def main():
     ap.add_argument("--cpu-baseline-tokens", type=int, default=2)
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--prof-steps", type=int, default=16)
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (CPU rehearsal)")
+    ap.add_argument("--device-map", default="", help="comma list: local rank -> HIP device (rehearsals "
+                                                     "that put several ranks on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.device_map:
+        local = [int(v) for v in args.device_map.split(",")][local]
 
     import torch
     import torch.distributed as dist
     from __graft_entry__ import _pkg
     _pkg()
     from hip_llama_cpp_amd import thallama as tl
+    from hip_llama_cpp_amd import dist as D
 
     if tl.device_count() < 1:
         raise SystemExit("bench.py: no HIP device")
     torch.cuda.set_device(local)
     tl.check(tl.lib().thallama_set_device(local))
     if world > 1:
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend=args.dist_backend)
 
     cfg_t, shared, mname = MODELS[args.model]
     c = tl.Config.make(*cfg_t)
@@ -83,9 +92,7 @@ def main():
     if world > 1:
         dist.barrier()
         tb = time.perf_counter()
-        chunk = 1 << 28  # 1 GiB of fp32 per collective
-        for s in range(0, n_floats, chunk):
-            dist.broadcast(arena[s:s + chunk], src=0)
+        D.broadcast_arena(arena, src=0)
         torch.cuda.synchronize()
         t_bcast = time.perf_counter() - tb
     t_init = time.perf_counter() - t0
@@ -114,10 +121,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = D.max_over_ranks(elapsed, device=f"cuda:{local}")
     tokens = world * B * K
     value = tokens / elapsed
     ms_step = elapsed / K * 1e3

@@ -113,6 +113,158 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Wave-level decode attention: one 64-lane wave (= one 64-thread block) per
+// (sequence b, head h, unit s), NS units per (b, h).  Unit s walks key chunks
+// c = s, s+NS, s+2NS, ... of CH keys; for every chunk the K rows AND the V rows
+// are requested together (one memory latency per chunk, not three), the
+// scores go through a 32-float LDS strip, and chunks are merged with an online
+// softmax.  No block barriers: max/sum are wave reductions.
+//  * if the context fits one chunk (T <= CH) unit 0 alone computes the reference
+//    order exactly (normalise the probabilities, then sum) and writes the output;
+//  * otherwise each live unit publishes (o, m, l) with write-through (sc1)
+//    stores, drains them (s_waitcnt vmcnt(0)) and takes a ticket from an
+//    agent-scope atomic counter; the unit that draws the last ticket reads every
+//    partial with sc1 loads, combines them and re-arms the counter
+//    (MI355X_MICROARCH.md §visibility, "Valid forms", row 1: no fences needed).
+// Units are numbered s-major (blockIdx = s*B*H + b*H + h) so the live ones at short
+// contexts are the lowest block ids and spread over every CU.
+struct AttnWaveParams {
+  AttnParams a;
+  unsigned* cnt;  // [B*H] tickets, zero between launches
+  int B, NS;
+};
+
+TL_DEVICE void st_sc1(float* p, float v) {
+  __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+TL_DEVICE float ld_sc1(const float* p) {
+  return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT));
+}
+
+template <int HS, int CH>
+__global__ void __launch_bounds__(64) attn_wave_kernel(AttnWaveParams w) {
+  constexpr int LPK = HS / 4;    // lanes per key row (one float4 each)
+  constexpr int KPI = 64 / LPK;  // keys per wave-instruction
+  constexpr int NI = CH / KPI;   // K wave-loads per chunk
+  constexpr int VPL = HS / 64;   // output columns per lane
+  static_assert(CH <= 64 && HS % 64 == 0, "chunk <= 64 keys, head size multiple of 64");
+  __shared__ float sc[64];
+  const AttnParams& p = w.a;
+  const int lane = threadIdx.x;
+  const int BH = w.B * p.n_heads;
+  const int s = blockIdx.x / BH, bh = blockIdx.x % BH;
+  const int b = bh / p.n_heads, h = bh % p.n_heads;
+  const int T = p.pos[b] + 1;
+  const int nchunks = (T + CH - 1) / CH;
+  const int nact = nchunks < w.NS ? nchunks : w.NS;  // live units for this (b, h)
+  if (s >= nact) return;
+
+  const int kvh = h / p.kv_mul;
+  const float* kbase = p.kc + (long long)b * p.kv_b_stride + p.kv_l_off + (long long)kvh * HS;
+  const float* vbase = p.vc + (long long)b * p.kv_b_stride + p.kv_l_off + (long long)kvh * HS;
+  const f4 qv = reinterpret_cast<const f4*>(p.q + (long long)b * p.dim + h * HS)[lane % LPK];
+  const float rs = sqrtf((float)HS);
+  const bool whole = nchunks == 1;
+
+  float m = -3.402823466e+38f, l = 0.f;
+  float o[VPL];
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) o[c] = 0.f;
+
+  for (int ch = s; ch < nchunks; ch += w.NS) {
+    const int t0 = ch * CH, t1 = min(T, t0 + CH), n = t1 - t0;
+    // K and V rows of the chunk, all in flight at once (rows past the chunk are
+    // clamped to its last row: loaded, weighted by 0)
+    f4 kv[NI];
+    float vv[CH][VPL];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int t = min(t0 + i * KPI + lane / LPK, t1 - 1);
+      kv[i] = reinterpret_cast<const f4*>(kbase + (long long)t * p.kv_dim)[lane % LPK];
+    }
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const float* vr = vbase + (long long)min(t0 + u, t1 - 1) * p.kv_dim + lane * VPL;
+#pragma unroll
+      for (int c = 0; c < VPL; ++c) vv[u][c] = vr[c];
+    }
+    // scores (reference src/seq.cpp:107-117)
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const float d = group_sum<LPK>(dot4(qv, kv[i], 0.f));
+      const int t = i * KPI + lane / LPK;
+      if ((lane % LPK) == 0 && t < n) sc[t] = __fdiv_rn(d, rs);
+    }
+    __syncthreads();  // one-wave block: orders the score strip
+    const float my = lane < n ? sc[lane] : -3.402823466e+38f;
+    __syncthreads();  // the strip is rewritten by the next chunk
+    const float mc = wave_max(my);
+    float pr;
+    if (whole) {
+      // reference softmax (src/seq.cpp:18-36): exp, sum, divide, then the weighted sum
+      const float e = lane < n ? expf(__fsub_rn(my, mc)) : 0.f;
+      pr = __fdiv_rn(e, wave_sum(e));
+      m = mc;
+    } else {
+      const float mn = fmaxf(m, mc);
+      const float e = lane < n ? expf(__fsub_rn(my, mn)) : 0.f;
+      const float scale = expf(__fsub_rn(m, mn));  // rescale what earlier chunks summed
+      l = fmaf(l, scale, wave_sum(e));
+#pragma unroll
+      for (int c = 0; c < VPL; ++c) o[c] *= scale;
+      m = mn;
+      pr = e;
+    }
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const float a = __shfl(pr, u, 64);
+#pragma unroll
+      for (int c = 0; c < VPL; ++c) o[c] = fmaf(a, vv[u][c], o[c]);
+    }
+  }
+
+  float* out = p.out + (long long)b * p.dim + h * HS + lane * VPL;
+  if (whole) {
+#pragma unroll
+    for (int c = 0; c < VPL; ++c) out[c] = o[c];
+    return;
+  }
+  // publish this unit's partial (write-through), drain, take a ticket
+  float* rec = p.part + ((long long)bh * w.NS + s) * (HS + 4);
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) st_sc1(rec + lane * VPL + c, o[c]);
+  if (lane == 0) {
+    st_sc1(rec + HS, m);
+    st_sc1(rec + HS + 1, l);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  unsigned ticket = 0;
+  if (lane == 0) ticket = __hip_atomic_fetch_add(w.cnt + bh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ticket = __shfl(ticket, 0, 64);
+  if (ticket != (unsigned)(nact - 1)) return;
+  // last unit: combine every partial (sc1 loads only)
+  const float* recs = p.part + (long long)bh * w.NS * (HS + 4);
+  float M = -3.402823466e+38f;
+  for (int k = 0; k < nact; ++k) M = fmaxf(M, ld_sc1(recs + k * (HS + 4) + HS));
+  float L = 0.f;
+  float acc[VPL];
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) acc[c] = 0.f;
+  for (int k = 0; k < nact; ++k) {
+    const float* r = recs + k * (HS + 4);
+    const float sk = expf(__fsub_rn(ld_sc1(r + HS), M));
+    L = fmaf(ld_sc1(r + HS + 1), sk, L);
+#pragma unroll
+    for (int c = 0; c < VPL; ++c) acc[c] = fmaf(ld_sc1(r + lane * VPL + c), sk, acc[c]);
+  }
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) out[c] = __fdiv_rn(acc[c], L);
+  if (lane == 0) __hip_atomic_store(w.cnt + bh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // out[b][h*hs + i] = sum_s o_s[i] e^{m_s-M} / sum_s l_s e^{m_s-M}
 __global__ void __launch_bounds__(256) attn_combine_kernel(AttnParams p) {
   const int h = blockIdx.x, b = blockIdx.y;

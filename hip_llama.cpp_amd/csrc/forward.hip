@@ -47,16 +47,42 @@ extern "C" const char* thallama_last_error(void) { return g_last_error.c_str(); 
 // ------------------------------------------------------------------ argmax + advance
 // next = argmax(logits[b]) with lowest-index ties (sample_argmax, reference
 // src/llama.cpp:275-286); then tok[b] = next, out[b*cap + pos[b]] = next, pos[b]++.
-__global__ void __launch_bounds__(256) k_argmax_advance(const float* logits, int V, int* tok, int* pos,
-                                                        int* out, int cap) {
-  __shared__ unsigned long long red[4];
+// One 1024-thread block per sequence; float4 loads, 8 in flight per thread, then a
+// (value, index) reduction that keeps the lower index on ties.
+__global__ void __launch_bounds__(1024) k_argmax_advance(const float* logits, int V, int* tok, int* pos,
+                                                         int* out, int cap) {
+  __shared__ unsigned long long red[16];
   const int b = blockIdx.x;
   const float* l = logits + (long long)b * V;
-  unsigned long long best = 0;
-  for (int i = threadIdx.x; i < V; i += 256) {
-    unsigned long long k = tl::argmax_pack(l[i], i);
-    best = k > best ? k : best;
+  float bv = -INFINITY;
+  int bi = 0x7FFFFFFF;
+  const bool vec = ((V & 3) == 0) && (((uintptr_t)l & 15) == 0);
+  if (vec) {
+    const f4* l4 = reinterpret_cast<const f4*>(l);
+    const int n4 = V >> 2;
+    for (int i0 = threadIdx.x; i0 < n4; i0 += 1024 * 8) {
+      f4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * 1024;
+        v[u] = i < n4 ? l4[i] : f4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = 4 * (i0 + u * 1024);
+        if (v[u].x > bv) { bv = v[u].x; bi = i; }
+        if (v[u].y > bv) { bv = v[u].y; bi = i + 1; }
+        if (v[u].z > bv) { bv = v[u].z; bi = i + 2; }
+        if (v[u].w > bv) { bv = v[u].w; bi = i + 3; }
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < V; i += 1024)
+      if (l[i] > bv) { bv = l[i]; bi = i; }
   }
+  // a thread's indices increase along its stream, so strict '>' kept its lowest; across
+  // threads the packed key orders by value, then by lower index
+  unsigned long long best = bi == 0x7FFFFFFF ? 0ull : tl::argmax_pack(bv, bi);
   for (int o = 32; o > 0; o >>= 1) {
     unsigned long long other = __shfl_xor(best, o, 64);
     best = other > best ? other : best;
@@ -64,8 +90,9 @@ __global__ void __launch_bounds__(256) k_argmax_advance(const float* logits, int
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int w = 1; w < 4; ++w) best = red[w] > best ? red[w] : best;
-    const int next = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
+    for (int w = 1; w < 16; ++w) best = red[w] > best ? red[w] : best;
+    // all-NaN logits: sample_argmax keeps index 0
+    const int next = best ? (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull)) : 0;
     const int p = pos[b];
     if (out && p < cap) out[(long long)b * cap + p] = next;
     tok[b] = next;
@@ -74,6 +101,8 @@ __global__ void __launch_bounds__(256) k_argmax_advance(const float* logits, int
 }
 
 // ------------------------------------------------------------------ decoder
+static constexpr int kAttnChunk = 32;  // keys per attention wave unit
+
 struct thallama_decoder {
   Config cfg;
   TransformerWeights w;
@@ -90,7 +119,8 @@ struct thallama_decoder {
   int* tok_h = nullptr;  // pinned staging
   int* pos_h = nullptr;
   float2* rope_d = nullptr;
-  float* part_d = nullptr;
+  float* part_d = nullptr;      // attention partials [B][H][<=16 units][hs+4]
+  unsigned* cnt_d = nullptr;    // attention combine tickets [B][H]
   int nsplit = 1;
   bool nt = true;
   bool use_graph = false;
@@ -155,9 +185,10 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
     return (int)hipErrorInvalidValue;
   }
   const Config& c = *cfg;
+  const int hs_ = c.n_heads > 0 ? c.dim / c.n_heads : 0;
   if (c.dim <= 0 || c.n_heads <= 0 || c.n_kv_heads <= 0 || c.dim % c.n_heads || c.n_heads % c.n_kv_heads ||
-      (c.dim / c.n_heads) % 8 || (c.dim / c.n_heads) > 512 || c.seq_len <= 0) {
-    g_last_error = "thallama_decoder_create: unsupported config (head_size must be a multiple of 8, <= 512)";
+      hs_ < 8 || hs_ > 256 || (hs_ & (hs_ - 1)) || c.seq_len <= 0) {
+    g_last_error = "thallama_decoder_create: unsupported config (head_size must be a power of two in [8, 256])";
     return (int)hipErrorInvalidValue;
   }
   thallama_decoder* d = new thallama_decoder();
@@ -199,7 +230,13 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
   TL_TRY(hipMalloc(&d->rope_d, rope.size() * sizeof(float2)));
   TL_TRY(hipMemcpy(d->rope_d, rope.data(), rope.size() * sizeof(float2), hipMemcpyHostToDevice));
   d->nsplit = auto_splits(d);
-  TL_TRY(hipMalloc(&d->part_d, sizeof(float) * (size_t)batch * d->H * 16 * (d->hs + 4)));
+  {
+    const size_t nsmax = (size_t)((d->S + kAttnChunk - 1) / kAttnChunk);
+    const size_t recs = (size_t)batch * d->H * (nsmax > 16 ? nsmax : 16);
+    TL_TRY(hipMalloc(&d->part_d, sizeof(float) * recs * (d->hs + 4)));
+    TL_TRY(hipMalloc(&d->cnt_d, sizeof(unsigned) * (size_t)batch * d->H));
+    TL_TRY(hipMemset(d->cnt_d, 0, sizeof(unsigned) * (size_t)batch * d->H));
+  }
   // weights far beyond the 256 MiB Infinity Cache stream once per step: nt loads
   const double wbytes = 4.0 * ((double)d->L * (2.0 * d->dim * d->dim + 2.0 * d->dim * d->kv_dim +
                                                3.0 * d->dim * d->hidden) + (double)d->V * d->dim);
@@ -220,6 +257,7 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   (void)hipHostFree(d->pos_h);
   (void)hipFree(d->rope_d);
   (void)hipFree(d->part_d);
+  (void)hipFree(d->cnt_d);
   if (d->own_stream) (void)hipStreamDestroy(d->stream);
   delete d;
 }
@@ -304,7 +342,25 @@ static int enqueue_step(thallama_decoder* d) {
       const int lpk = d->hs / 4;
       const size_t lds = 64 + (size_t)(S > 1024 ? S : 1024) * 4;
       int ev = prof_begin(d);
-      dim3 grid(d->H, d->B, d->nsplit);
+      if (d->hs == 64 || d->hs == 128 || d->hs == 256) {
+        // wave-level units, in-kernel combine (attention.hpp: attn_wave_kernel)
+        tl::AttnWaveParams wp;
+        wp.a = a;
+        wp.cnt = d->cnt_d;
+        wp.B = d->B;
+        const int max_chunks = (S + kAttnChunk - 1) / kAttnChunk;
+        wp.NS = d->nsplit < max_chunks ? d->nsplit : max_chunks;
+        const int units = d->B * d->H * wp.NS;
+        if (d->hs == 64)
+          hipLaunchKernelGGL((tl::attn_wave_kernel<64, kAttnChunk>), dim3(units), dim3(64), 0, d->stream, wp);
+        else if (d->hs == 128)
+          hipLaunchKernelGGL((tl::attn_wave_kernel<128, kAttnChunk>), dim3(units), dim3(64), 0, d->stream, wp);
+        else  // half-size chunks keep head-256 K/V rows in registers without spills
+          hipLaunchKernelGGL((tl::attn_wave_kernel<256, kAttnChunk / 2>), dim3(units), dim3(64), 0, d->stream, wp);
+        TL_TRY(hipGetLastError());
+      } else {
+        // generic head sizes: block kernel + separate combine launch
+        dim3 grid(d->H, d->B, d->nsplit);
       switch (lpk) {
         case 2: hipLaunchKernelGGL(tl::attn_decode_kernel<2>, grid, dim3(256), lds, d->stream, a); break;
         case 4: hipLaunchKernelGGL(tl::attn_decode_kernel<4>, grid, dim3(256), lds, d->stream, a); break;
@@ -320,6 +376,7 @@ static int enqueue_step(thallama_decoder* d) {
       if (d->nsplit > 1) {
         hipLaunchKernelGGL(tl::attn_combine_kernel, dim3(d->H, d->B), dim3(128), 0, d->stream, a);
         TL_TRY(hipGetLastError());
+      }
       }
       prof_end(d, THALLAMA_K_ATTN, ev);
     }
@@ -397,7 +454,7 @@ static int enqueue_step(thallama_decoder* d) {
 
 static int enqueue_argmax(thallama_decoder* d) {
   int ev = prof_begin(d);
-  hipLaunchKernelGGL(k_argmax_advance, dim3(d->B), dim3(256), 0, d->stream, d->s.logits, d->V, d->tok_d,
+  hipLaunchKernelGGL(k_argmax_advance, dim3(d->B), dim3(1024), 0, d->stream, d->s.logits, d->V, d->tok_d,
                      d->pos_d, d->out_d, d->S);
   TL_TRY(hipGetLastError());
   prof_end(d, THALLAMA_K_ARGMAX, ev);

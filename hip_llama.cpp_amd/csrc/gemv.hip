@@ -17,64 +17,49 @@ bool gemv_fast_ok(const GemvParams& p) {
   return true;
 }
 
-template <int MODE, int NB>
-static hipError_t launch_nb(const GemvParams& p, hipStream_t s, bool nt) {
-  // LDS: 320 B of reduction scratch + NB x kc floats of staged activations.
-  // 64 KiB for the staged activations keeps >= 2 blocks per CU resident.
-  constexpr int kBudgetFloats = 16384;
-  int kc = (kBudgetFloats / NB) & ~255;
-  if (kc > p.K) kc = p.K;
-  const size_t lds = 320 + (size_t)NB * kc * 4;
-  constexpr int IPW = 1;
-  const int blocks = (p.n_items + 4 * IPW - 1) / (4 * IPW);
-  if (blocks <= 0) return hipSuccess;
-  if (nt)
-    hipLaunchKernelGGL((gemv_kernel<MODE, NB, IPW, true>), dim3(blocks), dim3(256), lds, s, p, kc);
-  else
-    hipLaunchKernelGGL((gemv_kernel<MODE, NB, IPW, false>), dim3(blocks), dim3(256), lds, s, p, kc);
-  return hipGetLastError();
+// Measured on MI355X (profiles/r01_gemv_sweep.json, llama2-7B shapes, weights streamed
+// from HBM): prefetch-before-staging costs 64 VGPRs and loses occupancy everywhere
+// (-2..-12 %); non-temporal weight loads win 5-10 %; at NB = 1 one item per wave is
+// best except the K = 11008 down-projection (2 items, 8 waves: the 44 KiB staged
+// activation is amortised over twice the rows); for NB > 1 two items per wave halve
+// the LDS activation reads per weight byte.
+GemvCfg gemv_default_cfg(int mode, int n_items, int K, int nb, bool nt) {
+  GemvCfg c;
+  c.nt = nt;
+  c.pf = false;
+  (void)mode;
+  (void)n_items;
+  if (nb == 1) {
+    c.ipw = K > 8192 ? 2 : 1;
+    c.waves = (K > 8192 || mode != GM_SWIGLU) ? 8 : 4;
+  } else {
+    c.ipw = 2;
+    c.waves = 4;
+  }
+  return c;
 }
 
-template <int MODE>
-static hipError_t launch_mode(const GemvParams& p0, hipStream_t s, bool nt) {
-  if (p0.n_items <= 0 || p0.nb <= 0) return hipSuccess;
-  if (!gemv_fast_ok(p0)) {
-    const int blocks = (p0.n_items + 3) / 4;
-    hipLaunchKernelGGL((gemv_generic_kernel<MODE>), dim3(blocks, p0.nb), dim3(256), 0, s, p0);
-    return hipGetLastError();
+hipError_t launch_mode_store(const GemvParams&, hipStream_t, const GemvCfg*, bool);
+hipError_t launch_mode_resid(const GemvParams&, hipStream_t, const GemvCfg*, bool);
+hipError_t launch_mode_swiglu(const GemvParams&, hipStream_t, const GemvCfg*, bool);
+hipError_t launch_mode_qkv(const GemvParams&, hipStream_t, const GemvCfg*, bool);
+
+static hipError_t dispatch(int mode, const GemvParams& p, hipStream_t s, const GemvCfg* cfg, bool nt) {
+  switch (mode) {
+    case GM_STORE: return launch_mode_store(p, s, cfg, nt);
+    case GM_RESID: return launch_mode_resid(p, s, cfg, nt);
+    case GM_SWIGLU: return launch_mode_swiglu(p, s, cfg, nt);
+    case GM_QKV: return launch_mode_qkv(p, s, cfg, nt);
   }
-  for (int b0 = 0; b0 < p0.nb; b0 += 16) {
-    GemvParams p = p0;
-    p.nb = p0.nb - b0 < 16 ? p0.nb - b0 : 16;
-    if (b0) {
-      if (p.x) p.x += b0 * p.x_stride;
-      if (p.tok) p.tok += b0;
-      if (p.x_out) p.x_out += b0 * p.x_stride;
-      if (p.pos) p.pos += b0;
-      if (MODE == GM_STORE) p.y_off += (long long)b0 * p.y_stride;
-      else p.y += (long long)b0 * p.y_stride;
-      if (p.kc) p.kc += (long long)b0 * p.kv_b_stride;
-      if (p.vc) p.vc += (long long)b0 * p.kv_b_stride;
-    }
-    hipError_t e;
-    if (p.nb == 1) e = launch_nb<MODE, 1>(p, s, nt);
-    else if (p.nb == 2) e = launch_nb<MODE, 2>(p, s, nt);
-    else if (p.nb <= 4) e = launch_nb<MODE, 4>(p, s, nt);
-    else if (p.nb <= 8) e = launch_nb<MODE, 8>(p, s, nt);
-    else e = launch_nb<MODE, 16>(p, s, nt);
-    if (e != hipSuccess) return e;
-  }
-  return hipSuccess;
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_gemv(int mode, const GemvParams& p, hipStream_t s, bool nt) {
-  switch (mode) {
-    case GM_STORE: return launch_mode<GM_STORE>(p, s, nt);
-    case GM_RESID: return launch_mode<GM_RESID>(p, s, nt);
-    case GM_SWIGLU: return launch_mode<GM_SWIGLU>(p, s, nt);
-    case GM_QKV: return launch_mode<GM_QKV>(p, s, nt);
-  }
-  return hipErrorInvalidValue;
+  return dispatch(mode, p, s, nullptr, nt);
+}
+
+hipError_t launch_gemv_cfg(int mode, const GemvParams& p, hipStream_t s, const GemvCfg& cfg) {
+  return dispatch(mode, p, s, &cfg, cfg.nt);
 }
 
 }  // namespace tl

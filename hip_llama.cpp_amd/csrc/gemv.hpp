@@ -146,10 +146,20 @@ TL_DEVICE void rms_scales(const GemvParams& p, float* ss, float* red) {
 }
 
 // Accumulate one row chunk: acc[b] += sum_j W[j*64+lane] . xs[b][j*64+lane], j < cnt.
-template <int NB, bool NT>
-TL_DEVICE void row_chunk(const f4* __restrict__ w, const f4* xs, int n4, int cnt, int lane,
-                         float (&acc)[NB]) {
+// HASPRE: the first 16 wave-loads were issued earlier (before the activation staging
+// barrier) and arrive in `pre`.
+template <int NB, bool NT, bool HASPRE>
+TL_DEVICE void row_chunk(const f4* __restrict__ w, const f4* xs, int n4, int cnt, int lane, float (&acc)[NB],
+                         const f4 (&pre)[16]) {
   int j = 0;
+  if constexpr (HASPRE) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b) acc[b] = dot4(pre[u], xs[b * n4 + u * 64 + lane], acc[b]);
+    }
+    j = 16;
+  }
   for (; j + 16 <= cnt; j += 16) {
     f4 wv[16];
 #pragma unroll
@@ -236,16 +246,18 @@ TL_DEVICE void epilogue(const GemvParams& p, int item, const float (&v)[2][NB], 
   }
 }
 
-// WAVES waves per block, IPW items per wave, KC floats of x staged per chunk.
-template <int MODE, int NB, int IPW, bool NT>
-__global__ void __launch_bounds__(256) gemv_kernel(GemvParams p, int kc_max) {
+// WAVES waves per block, IPW items per wave, up to kc_max floats of x staged per chunk.
+// PF: when the activations fit one chunk, each wave issues its first row's first 16
+// wave-loads BEFORE staging, so the staging (L2 reads + RMSNorm + barrier) hides under
+// the weight stream's HBM latency.
+template <int MODE, int NB, int IPW, bool NT, int WAVES, bool PF>
+__global__ void __launch_bounds__(WAVES * 64) gemv_kernel(GemvParams p, int kc_max) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* red = reinterpret_cast<float*>(smem);          // 16 floats (block reductions)
   float* ss = red + 16;                                  // NB floats
   f4* xs = reinterpret_cast<f4*>(smem + 16 * 4 + 64 * 4); // [NB][kc/4]
 
   constexpr int RPI = RowsPerItem<MODE>::v;
-  constexpr int WAVES = 4;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int item0 = blockIdx.x * (WAVES * IPW) + wave;
@@ -260,6 +272,13 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemvParams p, int kc_max) {
 
   const int K = p.K;
   const bool single = K <= kc_max;
+  f4 pre[16];
+  const bool use_pre = PF && single && (K >> 8) >= 16 && item0 < p.n_items;
+  if (PF && use_pre) {
+    const f4* w = reinterpret_cast<const f4*>(item_row<MODE>(p, item0, 0));
+#pragma unroll
+    for (int u = 0; u < 16; ++u) pre[u] = load_w4<NT>(w + u * 64 + lane);
+  }
   if (p.rms_w && !single) rms_scales<NB>(p, ss, red);
 
   for (int kc = 0; kc < K; kc += kc_max) {
@@ -276,7 +295,10 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemvParams p, int kc_max) {
 #pragma unroll
         for (int r = 0; r < RPI; ++r) {
           const f4* w = reinterpret_cast<const f4*>(item_row<MODE>(p, item, r) + kc);
-          row_chunk<NB, NT>(w, xs, n4, cnt, lane, acc[i][r]);
+          if (PF && i == 0 && r == 0 && use_pre)
+            row_chunk<NB, NT, true>(w, xs, n4, cnt, lane, acc[i][r], pre);
+          else
+            row_chunk<NB, NT, false>(w, xs, n4, cnt, lane, acc[i][r], pre);
         }
       }
     }

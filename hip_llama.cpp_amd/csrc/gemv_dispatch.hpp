@@ -6,12 +6,26 @@
 
 namespace tl {
 
+// Launch shape of the streaming kernel.  ipw: items per wave; waves: waves per block;
+// pf: prefetch the first row before staging; nt: non-temporal weight loads;
+// lds_floats: activation staging budget (floats) per block.
+struct GemvCfg {
+  int ipw = 1;
+  int waves = 4;
+  bool pf = true;
+  bool nt = true;
+  int lds_floats = 16384;
+};
+
+// Tuned default for a shape (see tools/gemv_sweep.py and DESIGN.md §GEMV).
+GemvCfg gemv_default_cfg(int mode, int n_items, int K, int nb, bool nt);
+
 // True when the streaming kernel can take this shape: rows are a whole number of
 // 1-KiB wave-loads and every base pointer is 16-B aligned.
 bool gemv_fast_ok(const GemvParams& p);
 
 // Enqueue y = W x' for p.nb sequences on `stream` with epilogue `mode`.
-// nt: non-temporal weight loads.  Returns hipSuccess or the launch error.
 hipError_t launch_gemv(int mode, const GemvParams& p, hipStream_t stream, bool nt);
+hipError_t launch_gemv_cfg(int mode, const GemvParams& p, hipStream_t stream, const GemvCfg& cfg);
 
 }  // namespace tl

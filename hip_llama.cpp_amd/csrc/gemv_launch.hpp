@@ -1,0 +1,85 @@
+// gemv_launch.hpp — launch templates of the streaming GEMV, instantiated one epilogue
+// mode per translation unit (gemv_m*.hip) so the variants compile in parallel.
+#pragma once
+#include "gemv_dispatch.hpp"
+
+namespace tl {
+
+template <int MODE, int NB, int IPW, bool NT, int WAVES, bool PF>
+inline void launch_one(const GemvParams& p, hipStream_t s, int kc, size_t lds) {
+  const int per_block = WAVES * IPW;
+  const int blocks = (p.n_items + per_block - 1) / per_block;
+  hipLaunchKernelGGL((gemv_kernel<MODE, NB, IPW, NT, WAVES, PF>), dim3(blocks), dim3(WAVES * 64), lds, s, p, kc);
+}
+
+// Variant table: NB = 1 gets the full (ipw, waves, pf, nt) space for tuning; larger NB the
+// (ipw, pf, nt) space at 4 waves.
+template <int MODE, int NB>
+inline hipError_t launch_nb(const GemvParams& p, hipStream_t s, const GemvCfg& c) {
+  int kc = (c.lds_floats / NB) & ~255;
+  if (kc < 256) kc = 256;
+  if (kc > p.K) kc = p.K;
+  const size_t lds = 320 + (size_t)NB * kc * 4;
+  if (p.n_items <= 0) return hipSuccess;
+#define TL_L(IPW, NT, W, PF) launch_one<MODE, NB, IPW, NT, W, PF>(p, s, kc, lds)
+  const int ipw = c.ipw >= 2 ? 2 : 1;
+  bool done = false;
+  if constexpr (NB == 1) {
+    if (c.waves == 8) {
+      done = true;
+      if (ipw == 1) {
+        if (c.nt) { if (c.pf) TL_L(1, true, 8, true); else TL_L(1, true, 8, false); }
+        else { if (c.pf) TL_L(1, false, 8, true); else TL_L(1, false, 8, false); }
+      } else {
+        if (c.nt) { if (c.pf) TL_L(2, true, 8, true); else TL_L(2, true, 8, false); }
+        else { if (c.pf) TL_L(2, false, 8, true); else TL_L(2, false, 8, false); }
+      }
+    }
+  }
+  if (!done) {
+    if (ipw == 1) {
+      if (c.nt) { if (c.pf) TL_L(1, true, 4, true); else TL_L(1, true, 4, false); }
+      else { if (c.pf) TL_L(1, false, 4, true); else TL_L(1, false, 4, false); }
+    } else {
+      if (c.nt) { if (c.pf) TL_L(2, true, 4, true); else TL_L(2, true, 4, false); }
+      else { if (c.pf) TL_L(2, false, 4, true); else TL_L(2, false, 4, false); }
+    }
+  }
+#undef TL_L
+  return hipGetLastError();
+}
+
+template <int MODE>
+inline hipError_t launch_mode(const GemvParams& p0, hipStream_t s, const GemvCfg* cfg, bool nt) {
+  if (p0.n_items <= 0 || p0.nb <= 0) return hipSuccess;
+  if (!gemv_fast_ok(p0)) {
+    const int blocks = (p0.n_items + 3) / 4;
+    hipLaunchKernelGGL((gemv_generic_kernel<MODE>), dim3(blocks, p0.nb), dim3(256), 0, s, p0);
+    return hipGetLastError();
+  }
+  for (int b0 = 0; b0 < p0.nb; b0 += 16) {
+    GemvParams p = p0;
+    p.nb = p0.nb - b0 < 16 ? p0.nb - b0 : 16;
+    if (b0) {
+      if (p.x) p.x += b0 * p.x_stride;
+      if (p.tok) p.tok += b0;
+      if (p.x_out) p.x_out += b0 * p.x_stride;
+      if (p.pos) p.pos += b0;
+      if (MODE == GM_STORE) p.y_off += (long long)b0 * p.y_stride;
+      else p.y += (long long)b0 * p.y_stride;
+      if (p.kc) p.kc += (long long)b0 * p.kv_b_stride;
+      if (p.vc) p.vc += (long long)b0 * p.kv_b_stride;
+    }
+    const GemvCfg c = cfg ? *cfg : gemv_default_cfg(MODE, p.n_items, p.K, p.nb, nt);
+    hipError_t e;
+    if (p.nb == 1) e = launch_nb<MODE, 1>(p, s, c);
+    else if (p.nb == 2) e = launch_nb<MODE, 2>(p, s, c);
+    else if (p.nb <= 4) e = launch_nb<MODE, 4>(p, s, c);
+    else if (p.nb <= 8) e = launch_nb<MODE, 8>(p, s, c);
+    else e = launch_nb<MODE, 16>(p, s, c);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace tl

@@ -1,0 +1,8 @@
+// gemv_qkv.hip — GM_QKV instantiations of the streaming GEMV (gemv_launch.hpp).
+#include "gemv_launch.hpp"
+
+namespace tl {
+hipError_t launch_mode_qkv(const GemvParams& p, hipStream_t s, const GemvCfg* cfg, bool nt) {
+  return launch_mode<GM_QKV>(p, s, cfg, nt);
+}
+}  // namespace tl

@@ -1,0 +1,8 @@
+// gemv_swiglu.hip — GM_SWIGLU instantiations of the streaming GEMV (gemv_launch.hpp).
+#include "gemv_launch.hpp"
+
+namespace tl {
+hipError_t launch_mode_swiglu(const GemvParams& p, hipStream_t s, const GemvCfg* cfg, bool nt) {
+  return launch_mode<GM_SWIGLU>(p, s, cfg, nt);
+}
+}  // namespace tl

@@ -71,6 +71,13 @@ void thallama_decoder_prof_reset(thallama_decoder* d);
  * (weights once + KV rows read/written), used for roofline reporting. */
 double thallama_step_bytes(const Config* cfg, int batch, int kclass, const int* pos_h);
 
+/* Micro-benchmark of one streaming-GEMV launch shape (tools/gemv_sweep.py).  mode: 0 store,
+ * 1 residual, 2 SwiGLU (two MxK matrices), 3 QKV (dim = kv_dim = K, M ignored).  Variant:
+ * items per wave, waves per block, prefetch-before-staging, non-temporal loads.  Weights
+ * rotate over >= 1.5 GiB so every launch streams from HBM.  *us_out = avg us per launch. */
+int thallama_gemv_bench(int mode, int M, int K, int nb, int ipw, int waves, int pf, int nt, int iters,
+                        double* us_out);
+
 /* ---- synthetic weights ------------------------------------------------- */
 /* Fill a v0 arena (layout of thallama_map_weights) with the deterministic synthetic
  * model: N(0,0.02)-shaped linears/embedding, wo & w3 scaled by 1/sqrt(2L), norms 1,

@@ -62,6 +62,25 @@ def test_forced_logits_every_step(gpu, oracle, cfg, shared):
         assert int(np.argmax(got)) == oracle.lib().oracle_argmax(oracle.fp(want), cfg[5])
 
 
+@pytest.mark.parametrize("cfg", [
+    (256, 768, 2, 4, 4, 1024, 1024),    # head 64
+    (512, 1024, 2, 4, 2, 1024, 1024),   # head 128, GQA
+    (1024, 2048, 1, 4, 4, 512, 512),    # head 256
+    (128, 512, 2, 4, 4, 512, 512),      # head 32: block kernel + combine launch
+])
+def test_long_context_attention(gpu, oracle, cfg):
+    """Teacher-forced decode far past one attention chunk (32 keys): exercises the
+    multi-chunk path whose last-arriving chunk combines the partials in-kernel."""
+    c, model, state, dec, ref = build(gpu, oracle, cfg, 0, seed=21)
+    n = min(cfg[6], 700)
+    toks = np.random.default_rng(8).integers(0, cfg[5], n)
+    for p, t in enumerate(toks):
+        want = ref.forward(int(t), p)
+        got = dec.forward([int(t)], [p], want_logits=(p % 37 == 0 or p == n - 1))
+        if got is not None:
+            assert_ref_close(got[0], want, 1e-4, f"pos {p}")
+
+
 @pytest.mark.parametrize("B", [2, 3, 8])
 def test_batch_independent_positions(gpu, oracle, B):
     """B sequences at different positions in one step == B independent CPU decodes."""
