@@ -3,13 +3,15 @@
 
 One "step" = one greedy decode token for the B sequences a GPU holds, running the whole
 thaDNN forward (all layers, classifier, on-device argmax feeding the next token).
-Workload (N=1 line): llama2-7B-shaped fp32 model with random-init synthetic weights,
-BOS-started greedy decode over positions 0..K-1 (BASELINE.json configs[2]).
-Multi-GPU: one process per GPU (torch.distributed.run), each decodes its own independent
-prompts (weak scaling, no collective on the data path); rank 0 synthesises the weights and
-RCCL-broadcasts them over xGMI once at start-up.
+Default workload (the N=1 line): llama2-7B-shaped fp32 model, random-init synthetic weights,
+one BOS-started greedy sequence per GPU over positions 0..K-1 (BASELINE.json configs[2]).
+Other configs: --dtype int8 (configs[3], runq Q8_0 layout), --batch 8 (configs[4] per GPU),
+--model 110m (configs[1]).
+Multi-GPU: one process per GPU (torch.distributed.run); each rank decodes its own
+independent sequences (weak scaling, no collective on the data path); rank 0 synthesises the
+weights once and RCCL-broadcasts them over xGMI.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--model 7b|110m] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model 7b|110m] [--dtype f32|int8] [--batch B]
 """
 import argparse
 import json
@@ -21,11 +23,12 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 MODELS = {
-    # (dim, hidden, layers, heads, kv_heads, vocab, seq_len), shared classifier
+    # (dim, hidden, layers, heads, kv_heads, vocab, seq_len), shared classifier, name
     "7b": ((4096, 11008, 32, 32, 32, 32000, 2048), 0, "llama2-7B"),
     "110m": ((768, 2048, 12, 12, 12, 32000, 1024), 1, "stories110M"),
 }
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+SEED = 20240224
 
 
 def log(*a):
@@ -38,6 +41,8 @@ def main():
     ap.add_argument("--steps", type=int, default=256)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--model", default="7b", choices=sorted(MODELS))
+    ap.add_argument("--dtype", default="f32", choices=["f32", "int8"])
+    ap.add_argument("--group-size", type=int, default=64, help="Q8_0 group size (int8)")
     ap.add_argument("--batch", type=int, default=1, help="sequences per GPU")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-nt", action="store_true")
@@ -46,8 +51,8 @@ def main():
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--prof-steps", type=int, default=16)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (CPU rehearsal)")
-    ap.add_argument("--device-map", default="", help="comma list: local rank -> HIP device (rehearsals "
-                                                     "that put several ranks on one GPU)")
+    ap.add_argument("--device-map", default="", help="comma list: local rank -> HIP device (rehearsals that "
+                                                     "put several ranks on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -72,31 +77,52 @@ def main():
             dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend=args.dist_backend)
+    dev = f"cuda:{local}"
 
     cfg_t, shared, mname = MODELS[args.model]
     c = tl.Config.make(*cfg_t)
     B, K, W = args.batch, args.steps, args.warmup
-    S = cfg_t[6]
+    S, L = cfg_t[6], cfg_t[2]
+    gs = args.group_size
     if K > S or W > S:
         raise SystemExit(f"--steps/--warmup must be <= seq_len {S}")
+    q8 = args.dtype == "int8"
 
-    # ---------------- weights: one arena, rank 0 synthesises, RCCL broadcast to the others
-    n_floats = tl.lib().thallama_v0_payload_floats(tl.C.byref(c), shared)
+    # ---------------- weights: rank 0 synthesises (and for int8 quantises, export.py
+    # semantics), then one RCCL broadcast of the packed weight image to every other rank
     t0 = time.perf_counter()
-    arena = torch.empty(n_floats, dtype=torch.float32, device=f"cuda:{local}")
-    if rank == 0 or world == 1:
-        tl.check(tl.lib().thallama_synth_arena(tl.C.cast(tl.C.c_void_p(arena.data_ptr()), tl.c_float_p),
-                                               tl.C.byref(c), shared, tl.C.c_uint64(20240224), None), "synth")
+    n_floats = tl.lib().thallama_v0_payload_floats(tl.C.byref(c), shared)
+    if not q8:
+        image = torch.empty(n_floats, dtype=torch.float32, device=dev)
+        if rank == 0:
+            tl.check(tl.lib().thallama_synth_arena(tl.C.cast(tl.C.c_void_p(image.data_ptr()), tl.c_float_p),
+                                                   tl.C.byref(c), shared, tl.C.c_uint64(SEED), None), "synth")
+    else:
+        nbytes = tl.lib().thallama_q8_payload_bytes(tl.C.byref(c), shared, gs)
+        image = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            fp = torch.empty(n_floats, dtype=torch.float32, device=dev)
+            tl.check(tl.lib().thallama_synth_arena(tl.C.cast(tl.C.c_void_p(fp.data_ptr()), tl.c_float_p),
+                                                   tl.C.byref(c), shared, tl.C.c_uint64(SEED), None), "synth")
+            fpm = tl.DeviceModel(c, shared, arena_ptr=fp.data_ptr())
+            tl.check(tl.lib().thallama_q8_quantize_model(tl.C.c_void_p(image.data_ptr()), tl.C.byref(fpm.w),
+                                                         tl.C.byref(c), shared, gs, None), "q8 quantize")
+            torch.cuda.synchronize()
+            del fpm, fp
+            torch.cuda.empty_cache()
     torch.cuda.synchronize()
     t_bcast = 0.0
     if world > 1:
         dist.barrier()
         tb = time.perf_counter()
-        D.broadcast_arena(arena, src=0)
+        D.broadcast_arena(image, src=0)
         torch.cuda.synchronize()
         t_bcast = time.perf_counter() - tb
     t_init = time.perf_counter() - t0
-    model = tl.DeviceModel(c, shared, arena_ptr=arena.data_ptr())
+    if q8:
+        model = tl.DeviceModelQ8(c, shared, gs, payload_ptr=image.data_ptr())
+    else:
+        model = tl.DeviceModel(c, shared, arena_ptr=image.data_ptr())
     state = tl.DeviceState(c, B)
     dec = tl.Decoder(model, state)
     dec.set(tl.OPT_USE_GRAPH, 0 if args.no_graph else 1)
@@ -104,11 +130,9 @@ def main():
         dec.set(tl.OPT_NT_WEIGHTS, 0)
     if args.splits:
         dec.set(tl.OPT_ATTN_SPLITS, args.splits)
-    log(f"[rank {rank}] model {mname} B={B} init {t_init:.2f}s (broadcast {t_bcast:.2f}s)")
+    log(f"[rank {rank}] {mname} {args.dtype} B={B} init {t_init:.2f}s (broadcast {t_bcast:.2f}s)")
 
-    tok0 = [1] * B  # BOS
-    pos0 = [0] * B
-    # ---------------- warmup
+    tok0, pos0 = [1] * B, [0] * B  # BOS at position 0
     if W:
         dec.greedy(tok0, pos0, W, want_tokens=False, sync=True)
     # ---------------- timed region: K greedy steps at positions 0..K-1
@@ -120,26 +144,21 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    elapsed = D.max_over_ranks(elapsed, device=f"cuda:{local}")
-    tokens = world * B * K
-    value = tokens / elapsed
+    elapsed = D.max_over_ranks(time.perf_counter() - t0, device=dev)
+    value = world * B * K / elapsed
     ms_step = elapsed / K * 1e3
 
-    # whole-step algorithmic bytes (weights once per step + KV read/written at each position)
-    positions = list(range(K))
-    step_bytes = 0.0
-    for p in positions:
-        pos = [p] * B
-        L = cfg_t[2]
-        step_bytes += L * sum(tl.step_bytes(c, B, k, pos) for k in (tl.K_QKV, tl.K_ATTN, tl.K_WO, tl.K_FFN_UP,
-                                                                      tl.K_FFN_DOWN))
-        step_bytes += tl.step_bytes(c, B, tl.K_CLS, pos) + tl.step_bytes(c, B, tl.K_ARGMAX, pos)
-    step_bytes /= K
+    # ---------------- algorithmic bytes per step: weights once + KV rows at each position
+    def launch_bytes(kclass, pos):
+        return tl.step_bytes_q8(c, B, kclass, pos, gs) if q8 else tl.step_bytes(c, B, kclass, pos)
+
+    layer_classes = (tl.K_QKV, tl.K_ATTN, tl.K_WO, tl.K_FFN_UP, tl.K_FFN_DOWN)
+    step_bytes = sum(L * sum(launch_bytes(k, [p] * B) for k in layer_classes) + launch_bytes(tl.K_CLS, [p] * B)
+                     + launch_bytes(tl.K_ARGMAX, [p] * B) for p in range(K)) / K
     step_gbs = step_bytes / (ms_step * 1e-3) / 1e9
 
-    # ---------------- dominant-kernel roofline: HIP events around every launch (eager replay of
-    # the same steps on the decoder's stream), averaged per kernel class
+    # ---------------- per-kernel-class timing: HIP events around every launch on the decoder's
+    # stream, over an eager replay of the first prof-steps positions
     prof = {}
     if rank == 0:
         P = min(args.prof_steps, K)
@@ -150,31 +169,35 @@ def main():
             ms, n = dec.prof(k)
             if n:
                 prof[name] = {"avg_us": 1e3 * ms / n, "launches": n}
+                if k not in (tl.K_ATTN, tl.K_ARGMAX):
+                    prof[name]["GBps"] = launch_bytes(k, [0] * B) / (prof[name]["avg_us"] * 1e-6) / 1e9
         dec.set(tl.OPT_PROFILE, 0)
-        ffn = prof.get("ffn_up", {})
-        bytes_ffn = tl.step_bytes(c, B, tl.K_FFN_UP, [0] * B)
-        if ffn:
-            prof["ffn_up"]["GBps"] = bytes_ffn / (ffn["avg_us"] * 1e-6) / 1e9
-        for name, k in (("qkv", tl.K_QKV), ("wo", tl.K_WO), ("ffn_down", tl.K_FFN_DOWN), ("cls", tl.K_CLS)):
-            if name in prof:
-                prof[name]["GBps"] = tl.step_bytes(c, B, k, [0] * B) / (prof[name]["avg_us"] * 1e-6) / 1e9
 
-    # ---------------- CPU baseline: the oracle's seq.cpp restatement, 1 core, same model shape
+    # ---------------- CPU baseline: the oracle (bit-exact seq.cpp / runq.c restatement), same model
     cpu = None
     if rank == 0 and world == 1 and not args.skip_cpu and args.cpu_baseline_tokens > 0:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle as O
-        O.set_threads(min(16, os.cpu_count() or 1))  # weight synthesis only
-        ref = O.Model(cfg_t, shared, seed=20240224)
-        O.set_threads(1)
+        threads = min(16, os.cpu_count() or 1)
+        O.set_threads(threads)  # weight synthesis (+ int8 quantisation) only
+        ref = O.Model(cfg_t, shared, seed=SEED)
         n = args.cpu_baseline_tokens
-        tc = time.perf_counter()
-        ctoks = ref.greedy(1, 0, n)
+        if q8:
+            ref.build_q8(gs)
+            cores = threads  # runq.c's matmul is OpenMP-parallel (runq.c:324)
+            tc = time.perf_counter()
+            ctoks = ref.q8_greedy(1, 0, n)
+        else:
+            O.set_threads(1)
+            cores = 1  # seq.cpp is single-threaded
+            tc = time.perf_counter()
+            ctoks = ref.greedy(1, 0, n)
         tcpu = time.perf_counter() - tc
-        gtoks = dec.greedy(tok0[:1] * B, pos0, n)[:, 0].tolist()
-        cpu = {"value": n / tcpu, "unit": "tok/s", "cores": 1, "kind": "port",
-               "sample": f"{n} greedy tokens from BOS (pos 0..{n - 1}) of the same synthetic {mname} fp32 model, "
-                         f"oracle/oracle.c (bit-exact seq.cpp restatement), single thread",
+        gtoks = dec.greedy([1] * B, pos0, n)[:, 0].tolist()
+        cpu = {"value": round(n / tcpu, 4), "unit": "tok/s", "cores": cores, "kind": "port",
+               "sample": f"{n} greedy tokens from BOS (pos 0..{n - 1}) of the same synthetic {mname} "
+                         f"{args.dtype} model with oracle/oracle.c (bit-exact "
+                         f"{'runq.c' if q8 else 'src/seq.cpp'} restatement), {cores} thread(s)",
                "tokens_match_gpu": ctoks == gtoks}
         ref.close()
 
@@ -182,26 +205,24 @@ def main():
         ffn = prof.get("ffn_up")
         roof = None
         if ffn:
-            achieved = ffn["GBps"]
-            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                    "kernel": "gemv_kernel<GM_SWIGLU> (RMSNorm + W1/W3 + SwiGLU)",
-                    "bytes_per_launch": tl.step_bytes(c, B, tl.K_FFN_UP, [0] * B),
-                    "avg_us": round(ffn["avg_us"], 2)}
+            roof = {"bound": "hbm", "achieved": round(ffn["GBps"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ffn["GBps"] / HBM_PEAK_GBS, 4), "traffic": None,
+                    "kernel": ("gemv_q8_kernel" if q8 else "gemv_kernel") + "<GM_SWIGLU> (RMSNorm + W1/W3 + SwiGLU)",
+                    "bytes_per_launch": launch_bytes(tl.K_FFN_UP, [0] * B), "avg_us": round(ffn["avg_us"], 2)}
         out = {
             "metric": "decode tokens/sec (greedy, whole model) + achieved HBM GB/s fraction",
             "value": round(value, 3), "unit": "tok/s", "n_gpus": world, "steps": K, "warmup": W,
-            "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32", "data": "synthetic (random-init weights, BOS-started greedy)",
-            "config": {"workload": f"{mname} fp32 decode, {B} seq/GPU, positions 0..{K - 1}", "model": mname,
-                       "global_batch": B * world, "seq_len": S, "parallelism": f"prompt-dp{world}"},
+            "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": args.dtype, "data": "synthetic (random-init weights, BOS-started greedy decode)",
+            "config": {"workload": f"{mname} {args.dtype} greedy decode, {B} seq/GPU, positions 0..{K - 1}",
+                       "model": mname, "global_batch": B * world, "seq_len": S, "parallelism": f"prompt-dp{world}"},
             "hbm": {"step_bytes": step_bytes, "achieved_GBps": round(step_gbs, 1),
                     "frac_of_peak": round(step_gbs / HBM_PEAK_GBS, 4),
                     "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / step_bytes * B * world, 1)},
             "roofline": roof,
             "kernels": {k: {kk: round(vv, 2) for kk, vv in v.items()} for k, v in prof.items()},
             "cpu_baseline": cpu,
-            "init_s": round(t_init, 2),
+            "init_s": round(t_init, 2), "broadcast_s": round(t_bcast, 2),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

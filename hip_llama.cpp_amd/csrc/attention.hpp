@@ -129,10 +129,12 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p) {
 //    (MI355X_MICROARCH.md §visibility, "Valid forms", row 1: no fences needed).
 // Units are numbered s-major (blockIdx = s*B*H + b*H + h) so the live ones at short
 // contexts are the lowest block ids and spread over every CU.
+constexpr int kMaxNS = 16;  // units per (b, h) at most
+
 struct AttnWaveParams {
   AttnParams a;
   unsigned* cnt;  // [B*H] tickets, zero between launches
-  int B, NS;
+  int B, NS;      // NS <= kMaxNS
 };
 
 TL_DEVICE void st_sc1(float* p, float v) {
@@ -245,20 +247,32 @@ __global__ void __launch_bounds__(64) attn_wave_kernel(AttnWaveParams w) {
   if (lane == 0) ticket = __hip_atomic_fetch_add(w.cnt + bh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   ticket = __shfl(ticket, 0, 64);
   if (ticket != (unsigned)(nact - 1)) return;
-  // last unit: combine every partial (sc1 loads only)
+  // last unit: combine every partial (sc1 loads only).  Lane k reads unit k's (m, l);
+  // every lane then reads its columns of all kMaxNS records at once (records past nact
+  // are clamped to the last live one and weighted 0), so the combine costs one memory
+  // latency instead of one per partial.
   const float* recs = p.part + (long long)bh * w.NS * (HS + 4);
-  float M = -3.402823466e+38f;
-  for (int k = 0; k < nact; ++k) M = fmaxf(M, ld_sc1(recs + k * (HS + 4) + HS));
-  float L = 0.f;
+  const int kl = lane < nact ? lane : nact - 1;
+  const float mk = ld_sc1(recs + kl * (HS + 4) + HS);
+  const float lk = ld_sc1(recs + kl * (HS + 4) + HS + 1);
+  float ov[kMaxNS][VPL];
+#pragma unroll
+  for (int k = 0; k < kMaxNS; ++k) {
+    const int kk = k < nact ? k : nact - 1;
+#pragma unroll
+    for (int c = 0; c < VPL; ++c) ov[k][c] = ld_sc1(recs + kk * (HS + 4) + lane * VPL + c);
+  }
+  const float M = wave_max(lane < nact ? mk : -3.402823466e+38f);
+  const float sk = lane < nact ? expf(__fsub_rn(mk, M)) : 0.f;
+  const float L = wave_sum(lk * sk);
   float acc[VPL];
 #pragma unroll
   for (int c = 0; c < VPL; ++c) acc[c] = 0.f;
-  for (int k = 0; k < nact; ++k) {
-    const float* r = recs + k * (HS + 4);
-    const float sk = expf(__fsub_rn(ld_sc1(r + HS), M));
-    L = fmaf(ld_sc1(r + HS + 1), sk, L);
 #pragma unroll
-    for (int c = 0; c < VPL; ++c) acc[c] = fmaf(ld_sc1(r + lane * VPL + c), sk, acc[c]);
+  for (int k = 0; k < kMaxNS; ++k) {
+    const float a = __shfl(sk, k, 64);
+#pragma unroll
+    for (int c = 0; c < VPL; ++c) acc[c] = fmaf(ov[k][c], a, acc[c]);
   }
 #pragma unroll
   for (int c = 0; c < VPL; ++c) out[c] = __fdiv_rn(acc[c], L);

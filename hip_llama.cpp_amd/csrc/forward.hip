@@ -26,8 +26,10 @@
 #include "../../include/thaDNN.hpp"
 #include "../../include/thallama.h"
 #include "../../include/hip_helper.hpp"
+#include "../../include/thaQ8.hpp"
 #include "attention.hpp"
 #include "gemv_dispatch.hpp"
+#include "q8_dispatch.hpp"
 
 using tl::f4;
 
@@ -121,6 +123,8 @@ struct thallama_decoder {
   float2* rope_d = nullptr;
   float* part_d = nullptr;      // attention partials [B][H][<=16 units][hs+4]
   unsigned* cnt_d = nullptr;    // attention combine tickets [B][H]
+  bool q8 = false;              // int8 (runq Q8_0) weights in w8; w then holds only norms + embedding
+  Q8TransformerWeights w8 = {};
   int nsplit = 1;
   bool nt = true;
   bool use_graph = false;
@@ -280,6 +284,22 @@ extern "C" int thallama_decoder_set(thallama_decoder* d, int key, int value) {
 
 extern "C" hipStream_t thallama_decoder_stream(thallama_decoder* d) { return d ? d->stream : nullptr; }
 
+// One GEMV launch: fp32 weights from p.W*, or — for an int8 decoder — the Q8_0 tensors
+// t0..t2 (runq layout) through the int8 kernel (gemv_q8.hpp).
+static hipError_t gemv(thallama_decoder* d, int mode, tl::GemvParams& p, const QuantizedTensor* t0,
+                       const QuantizedTensor* t1, const QuantizedTensor* t2) {
+  if (!d->q8) return tl::launch_gemv(mode, p, d->stream, d->nt);
+  p.Q0 = t0 ? t0->q : nullptr;
+  p.S0 = t0 ? t0->s : nullptr;
+  p.Q1 = t1 ? t1->q : nullptr;
+  p.S1 = t1 ? t1->s : nullptr;
+  p.Q2 = t2 ? t2->q : nullptr;
+  p.S2 = t2 ? t2->s : nullptr;
+  p.gs = d->w8.group_size;
+  return tl::launch_gemv_q8(mode, p, d->stream, d->nt);
+}
+#define Q8L(name) (d->q8 ? &d->w8.name[l] : nullptr)
+
 // Enqueue one decode step reading tok_d / pos_d; logits land in s.logits.
 static int enqueue_step(thallama_decoder* d) {
   const int dim = d->dim, hid = d->hidden, kvd = d->kv_dim, S = d->S;
@@ -317,7 +337,7 @@ static int enqueue_step(thallama_decoder* d) {
       p.head_size = d->hs;
       p.rope = d->rope_d;
       int ev = prof_begin(d);
-      TL_TRY(tl::launch_gemv(tl::GM_QKV, p, d->stream, d->nt));
+      TL_TRY(gemv(d, tl::GM_QKV, p, Q8L(wq), Q8L(wk), Q8L(wv)));
       prof_end(d, THALLAMA_K_QKV, ev);
     }
     // 2. attention
@@ -392,7 +412,7 @@ static int enqueue_step(thallama_decoder* d) {
       p.y = s.x;
       p.y_stride = dim;
       int ev = prof_begin(d);
-      TL_TRY(tl::launch_gemv(tl::GM_RESID, p, d->stream, d->nt));
+      TL_TRY(gemv(d, tl::GM_RESID, p, Q8L(wo), nullptr, nullptr));
       prof_end(d, THALLAMA_K_WO, ev);
     }
     // 4. RMSNorm(ffn) + W1/W3 + SwiGLU
@@ -409,7 +429,7 @@ static int enqueue_step(thallama_decoder* d) {
       p.y = s.hb;
       p.y_stride = hid;
       int ev = prof_begin(d);
-      TL_TRY(tl::launch_gemv(tl::GM_SWIGLU, p, d->stream, d->nt));
+      TL_TRY(gemv(d, tl::GM_SWIGLU, p, Q8L(w1), Q8L(w3), nullptr));
       prof_end(d, THALLAMA_K_FFN_UP, ev);
     }
     // 5. W2 + residual
@@ -424,7 +444,7 @@ static int enqueue_step(thallama_decoder* d) {
       p.y = s.x;
       p.y_stride = dim;
       int ev = prof_begin(d);
-      TL_TRY(tl::launch_gemv(tl::GM_RESID, p, d->stream, d->nt));
+      TL_TRY(gemv(d, tl::GM_RESID, p, Q8L(w2), nullptr, nullptr));
       prof_end(d, THALLAMA_K_FFN_DOWN, ev);
     }
   }
@@ -446,7 +466,7 @@ static int enqueue_step(thallama_decoder* d) {
     p.y = s.logits;
     p.y_stride = d->V;
     int ev = prof_begin(d);
-    TL_TRY(tl::launch_gemv(tl::GM_STORE, p, d->stream, d->nt));
+    TL_TRY(gemv(d, tl::GM_STORE, p, d->q8 ? d->w8.wcls : nullptr, nullptr, nullptr));
     prof_end(d, THALLAMA_K_CLS, ev);
   }
   return 0;
@@ -623,6 +643,57 @@ extern "C" thablasStatus_t thaDNN_s_forward_batch(thablasHandle_t handle1, thabl
   int r = thallama_decoder_forward(d, token, pos, logits_host);
   if (r) {
     fprintf(stderr, "thaDNN_s_forward_batch: %s\n", thallama_last_error());
+    return r == (int)hipErrorInvalidValue ? THABLAS_STATUS_INVALID_VALUE : THABLAS_STATUS_EXECUTION_FAILED;
+  }
+  return THABLAS_STATUS_SUCCESS;
+}
+
+// ------------------------------------------------------------------ int8 (runq Q8_0) decoder
+extern "C" int thallama_decoder_create_q8(thallama_decoder** out, const Config* cfg, const Q8TransformerWeights* w8,
+                                          const RunState* s, int batch, hipStream_t stream) {
+  if (!w8 || !w8->wq || !w8->wcls || !w8->token_embedding_table || w8->group_size <= 0) {
+    g_last_error = "thallama_decoder_create_q8: incomplete Q8 weights (map + dequantised embedding required)";
+    return (int)hipErrorInvalidValue;
+  }
+  TransformerWeights w = {};
+  w.token_embedding_table = w8->token_embedding_table;
+  w.rms_att_weight = w8->rms_att_weight;
+  w.rms_ffn_weight = w8->rms_ffn_weight;
+  w.rms_final_weight = w8->rms_final_weight;
+  const int r = thallama_decoder_create(out, cfg, &w, s, batch, stream);
+  if (r) return r;
+  (*out)->q8 = true;
+  (*out)->w8 = *w8;
+  return 0;
+}
+
+extern "C" thablasStatus_t thaDNN_q8_forward_batch(thablasHandle_t handle, int n_batches, Config* p,
+                                                   Q8TransformerWeights* w, RunState* s_batch, int token[], int pos[],
+                                                   float* logits_host) {
+  if (!p || !w || !s_batch || !token || !pos || !logits_host || n_batches <= 0) return THABLAS_STATUS_INVALID_VALUE;
+  int dev = 0;
+  CHECK_HIP(hipGetDevice(&dev));
+  DecKey key(dev, handle.calc_stream, (const void*)w->wq, (const void*)s_batch->key_cache, (const void*)s_batch->x,
+             n_batches, p->dim, p->n_layers, p->seq_len, -p->vocab_size - 1 /* int8 keyspace */);
+  thallama_decoder* d = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_dec_mu);
+    auto it = dec_cache().find(key);
+    if (it != dec_cache().end()) {
+      d = it->second;
+      d->w8 = *w;
+      d->s = *s_batch;
+    } else {
+      if (thallama_decoder_create_q8(&d, p, w, s_batch, n_batches, handle.calc_stream) != 0) {
+        fprintf(stderr, "thaDNN_q8_forward_batch: %s\n", thallama_last_error());
+        return THABLAS_STATUS_INVALID_VALUE;
+      }
+      dec_cache()[key] = d;
+    }
+  }
+  const int r = thallama_decoder_forward(d, token, pos, logits_host);
+  if (r) {
+    fprintf(stderr, "thaDNN_q8_forward_batch: %s\n", thallama_last_error());
     return r == (int)hipErrorInvalidValue ? THABLAS_STATUS_INVALID_VALUE : THABLAS_STATUS_EXECUTION_FAILED;
   }
   return THABLAS_STATUS_SUCCESS;

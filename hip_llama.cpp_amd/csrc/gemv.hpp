@@ -59,6 +59,10 @@ struct GemvParams {
   long long kv_l_off;    // l*S*kv_dim
   int dim, kv_dim, head_size;
   const float2* rope;    // [S][head_size/2] (cos, sin), computed on the host with libm
+  // Q8_0 weights (gemv_q8.hpp): int8 rows + one fp32 scale per group of gs (runq.c:34-37)
+  const int8_t* Q0; const int8_t* Q1; const int8_t* Q2;
+  const float* S0; const float* S1; const float* S2;
+  int gs;
 };
 
 TL_DEVICE float silu_mul(float a, float b) {

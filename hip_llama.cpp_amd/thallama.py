@@ -59,6 +59,19 @@ class Transformer(C.Structure):
                 ("data", c_float_p), ("file_size", C.c_ssize_t)]
 
 
+class QuantizedTensor(C.Structure):
+    """runq.c:34-37 (include/thaQ8.hpp)"""
+    _fields_ = [("q", C.POINTER(C.c_int8)), ("s", c_float_p)]
+
+
+class Q8TransformerWeights(C.Structure):
+    """runq.c:39-59 field order (include/thaQ8.hpp)"""
+    _fields_ = [("q_tokens", C.POINTER(QuantizedTensor)), ("token_embedding_table", c_float_p),
+                ("rms_att_weight", c_float_p), ("rms_ffn_weight", c_float_p)] + \
+               [(n, C.POINTER(QuantizedTensor)) for n in ("wq", "wk", "wv", "wo", "w1", "w2", "w3")] + \
+               [("rms_final_weight", c_float_p), ("wcls", C.POINTER(QuantizedTensor)), ("group_size", C.c_int)]
+
+
 class Handle(C.Structure):
     """thablasHandle_t, reference include/thaBLAS.hpp:21-25"""
     _fields_ = [("current_gpu_id", C.c_int), ("calc_stream", C.c_void_p), ("copy_stream", C.c_void_p)]
@@ -116,6 +129,17 @@ def lib():
             "free_state_device": (None, [C.POINTER(RunState)]),
             "thallama_decoder_create": (I, [C.POINTER(VP), C.POINTER(Config), C.POINTER(TransformerWeights),
                                             C.POINTER(RunState), I, VP]),
+            "thallama_decoder_create_q8": (I, [C.POINTER(VP), C.POINTER(Config), C.POINTER(Q8TransformerWeights),
+                                               C.POINTER(RunState), I, VP]),
+            "thallama_q8_payload_bytes": (S, [C.POINTER(Config), I, I]),
+            "thallama_q8_map": (I, [C.POINTER(Q8TransformerWeights), C.POINTER(Config), VP, I, I, P]),
+            "thallama_q8_unmap": (None, [C.POINTER(Q8TransformerWeights)]),
+            "thallama_q8_dequant_embedding": (I, [C.POINTER(Q8TransformerWeights), C.POINTER(Config), VP]),
+            "thallama_q8_quantize_model": (I, [VP, C.POINTER(TransformerWeights), C.POINTER(Config), I, I, VP]),
+            "thaBLAS_q8_quantize_batch": (I, [C.POINTER(Handle), I, C.POINTER(C.c_int8), P, P, I, I, I]),
+            "thaBLAS_q8_matmul_batch": (I, [C.POINTER(Handle), I, P, P, C.POINTER(C.c_int8), P, I, I, I, I, I]),
+            "thaDNN_q8_forward_batch": (I, [Handle, I, C.POINTER(Config), C.POINTER(Q8TransformerWeights),
+                                            C.POINTER(RunState), c_int_p, c_int_p, P]),
             "thallama_decoder_destroy": (None, [VP]),
             "thallama_decoder_set": (I, [VP, I, I]),
             "thallama_decoder_stream": (VP, [VP]),
@@ -254,6 +278,55 @@ class DeviceModel:
         return out
 
 
+class DeviceModelQ8:
+    """int8 twin of a model (include/thaQ8.hpp): a device runq-v2 payload (norms fp32, Q8_0
+    tensors in export.py order) mapped like runq.c memory_map_weights, plus the dequantised
+    fp32 embedding table runq keeps (runq.c:199-201).
+
+    Built either by quantising a DeviceModel on the device (export.py semantics) or from a
+    host payload (e.g. the oracle's, or a v2 file minus its 256-byte header)."""
+
+    def __init__(self, cfg, shared, group_size=64, from_model=None, payload=None, payload_ptr=None):
+        self.cfg = cfg
+        self.shared = int(bool(shared))
+        self.gs = group_size
+        self.nbytes = lib().thallama_q8_payload_bytes(C.byref(cfg), self.shared, group_size)
+        self.buf = None
+        if payload_ptr is None:
+            self.buf = DevBuf(self.nbytes)
+            payload_ptr = self.buf.ptr
+        self.base = payload_ptr  # caller-owned when given (e.g. a torch tensor's data_ptr)
+        if from_model is not None:
+            check(lib().thallama_q8_quantize_model(C.c_void_p(self.base), C.byref(from_model.w), C.byref(cfg),
+                                                   self.shared, group_size, None), "q8 quantize")
+        elif payload is not None:
+            payload = np.ascontiguousarray(payload, np.uint8)
+            assert payload.size == self.nbytes, (payload.size, self.nbytes)
+            check(lib().thallama_memcpy_h2d(C.c_void_p(self.base), payload.ctypes.data_as(C.c_void_p), payload.nbytes))
+        self.emb = DevBuf(abs(cfg.vocab_size) * cfg.dim * 4)
+        self.w = Q8TransformerWeights()
+        check(lib().thallama_q8_map(C.byref(self.w), C.byref(cfg), C.c_void_p(self.base), self.shared, group_size,
+                                    self.emb.fptr()), "q8 map")
+        check(lib().thallama_q8_dequant_embedding(C.byref(self.w), C.byref(cfg), None), "q8 dequant")
+        sync()
+
+    def payload(self):
+        out = np.empty(self.nbytes, np.uint8)
+        check(lib().thallama_memcpy_d2h(out.ctypes.data_as(C.c_void_p), C.c_void_p(self.base), self.nbytes))
+        return out
+
+    def close(self):
+        if getattr(self, "w", None) is not None:
+            lib().thallama_q8_unmap(C.byref(self.w))
+            self.w = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class DeviceState:
     """Batched RunState (reference src/models.cpp:155-179)."""
 
@@ -287,8 +360,12 @@ class Decoder:
         self.cfg = model.cfg
         self.batch = batch or state.batch
         h = C.c_void_p()
-        check(lib().thallama_decoder_create(C.byref(h), C.byref(self.cfg), C.byref(model.w), C.byref(state.s),
-                                            self.batch, stream), "decoder_create")
+        if isinstance(model, DeviceModelQ8):
+            check(lib().thallama_decoder_create_q8(C.byref(h), C.byref(self.cfg), C.byref(model.w), C.byref(state.s),
+                                                   self.batch, stream), "decoder_create_q8")
+        else:
+            check(lib().thallama_decoder_create(C.byref(h), C.byref(self.cfg), C.byref(model.w), C.byref(state.s),
+                                                self.batch, stream), "decoder_create")
         self.h = h
 
     @property
@@ -346,3 +423,22 @@ class Decoder:
 def step_bytes(cfg, batch, kclass, pos):
     arr = (C.c_int * batch)(*[int(p) for p in pos])
     return lib().thallama_step_bytes(C.byref(cfg), batch, kclass, arr)
+
+
+def step_bytes_q8(cfg, batch, kclass, pos, gs):
+    """Algorithmic HBM bytes of one launch of kernel class kclass on the int8 path: int8 weights
+    + one fp32 scale per group, fp32 norms / activations / KV (as step_bytes)."""
+    dim, hid, V = cfg.dim, cfg.hidden_dim, abs(cfg.vocab_size)
+    kvd = cfg.kv_dim
+    qt = lambda n: n + 4 * n // gs  # noqa: E731
+    if kclass == K_QKV:
+        return qt(dim * dim + 2 * dim * kvd) + 4 * (dim + batch * (2 * dim + 2 * kvd))
+    if kclass == K_WO:
+        return qt(dim * dim) + 4 * batch * 3 * dim
+    if kclass == K_FFN_UP:
+        return qt(2 * hid * dim) + 4 * (dim + batch * (dim + hid))
+    if kclass == K_FFN_DOWN:
+        return qt(hid * dim) + 4 * batch * (hid + 2 * dim)
+    if kclass == K_CLS:
+        return qt(V * dim) + 4 * (dim + batch * (dim + V))
+    return step_bytes(cfg, batch, kclass, pos)

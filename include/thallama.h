@@ -18,6 +18,7 @@
 #include <stddef.h>
 #include <stdint.h>
 #include "models.hpp"
+#include "thaQ8.hpp"
 
 #ifdef __cplusplus
 extern "C" {
@@ -44,6 +45,10 @@ enum {
  * the decoder then creates its own non-blocking stream.  Returns 0 on success. */
 int thallama_decoder_create(thallama_decoder** out, const Config* cfg, const TransformerWeights* w,
                             const RunState* s, int batch, hipStream_t stream);
+/* Same, for int8 weights (include/thaQ8.hpp: a mapped v2 payload whose
+ * token_embedding_table has been dequantised). */
+int thallama_decoder_create_q8(thallama_decoder** out, const Config* cfg, const Q8TransformerWeights* w8,
+                               const RunState* s, int batch, hipStream_t stream);
 void thallama_decoder_destroy(thallama_decoder* d);
 int thallama_decoder_set(thallama_decoder* d, int key, int value);
 hipStream_t thallama_decoder_stream(thallama_decoder* d);

@@ -1,0 +1,119 @@
+"""GPU parity of the int8 (runq Q8_0) path against the CPU oracle's runq.c restatement
+(itself pinned to the reference runq.c in tests/test_oracle.py).
+
+* weight quantisation (export.py:46-70) and activation quantisation (runq.c:145-171):
+  bit-exact;
+* the fused quantise + int8 GEMV (runq.c:317-342): the int32 group sums are exact, the
+  fp32 sum over groups runs in a different order, so results are compared with the
+  reference tests' abs-or-rel rule at 1e-4;
+* the int8 decode step: greedy tokens identical; logits within 1e-3 abs-or-rel.  The
+  looser logit bound is inherent to runq's arithmetic, not to the kernels: the
+  activations are re-quantised before every matmul, so a last-bit difference in an fp32
+  activation (different summation order) can move one int8 code by 1 step (1/127 of the
+  group's max) and that step propagates.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from helpers import SMALL, SMALL_GQA, assert_ref_close, rng
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(tl, a):
+    return tl.DevBuf.from_array(np.ascontiguousarray(a))
+
+
+@pytest.mark.parametrize("cfg,shared,gs", [(SMALL, 0, 64), (SMALL_GQA, 0, 32), (SMALL, 1, 128)])
+def test_weight_quantisation_bitexact(gpu, oracle, cfg, shared, gs):
+    c = gpu.Config.make(*cfg)
+    m = gpu.DeviceModel(c, shared, seed=31)
+    q = gpu.DeviceModelQ8(c, shared, gs, from_model=m)
+    ref = oracle.Model(cfg, shared, seed=31)
+    ref.build_q8(gs)
+    np.testing.assert_array_equal(q.payload(), ref.q8_payload())
+
+
+@pytest.mark.parametrize("n,gs,B", [(4096, 64, 1), (11008, 64, 3), (768, 32, 2), (128, 128, 1)])
+def test_activation_quantisation_bitexact(gpu, handle, oracle, n, gs, B):
+    x = (rng(n).standard_normal((B, n)) * 0.7).astype(np.float32)
+    x[0, :gs] = 0.0  # an all-zero group: scale 0, codes 0 (runq divides by zero)
+    dx, dq, ds = dev(gpu, x), gpu.DevBuf(B * n), gpu.DevBuf(B * (n // gs) * 4)
+    assert gpu.lib().thaBLAS_q8_quantize_batch(C.byref(handle), B, C.cast(C.c_void_p(dq.ptr), C.POINTER(C.c_int8)),
+                                               ds.fptr(), dx.fptr(), n, gs, n) == 0
+    gpu.sync()
+    q = dq.download(np.int8).reshape(B, n)
+    s = ds.download(np.float32).reshape(B, n // gs)
+    for b in range(B):
+        qr, sr = oracle.q8_quantize(x[b], gs)
+        np.testing.assert_array_equal(s[b], sr)
+        np.testing.assert_array_equal(q[b], qr)
+
+
+@pytest.mark.parametrize("M,K,gs,B", [(4096, 4096, 64, 1), (4096, 11008, 64, 1), (768, 2048, 64, 4),
+                                      (1000, 768, 32, 2), (256, 1024, 128, 8), (64, 96, 32, 1)])
+def test_q8_matmul(gpu, handle, oracle, M, K, gs, B):
+    r = rng(M + K)
+    W = (r.standard_normal((M, K)) * 0.02).astype(np.float32)
+    wq, ws = oracle.q8_quantize_weights(W, gs)
+    X = r.standard_normal((B, K)).astype(np.float32)
+    dwq, dws, dX, dC = dev(gpu, wq), dev(gpu, ws), dev(gpu, X), gpu.DevBuf(B * M * 4)
+    assert gpu.lib().thaBLAS_q8_matmul_batch(C.byref(handle), B, dC.fptr(), dX.fptr(),
+                                             C.cast(C.c_void_p(dwq.ptr), C.POINTER(C.c_int8)), dws.fptr(), K, M, gs,
+                                             M, K) == 0
+    gpu.sync()
+    got = dC.download().reshape(B, M)
+    for b in range(B):
+        xq, xs = oracle.q8_quantize(X[b], gs)
+        want = oracle.q8_matmul(xq, xs, wq, ws, K, M, gs)
+        assert_ref_close(got[b], want, 1e-4, f"q8 matmul b={b}")
+
+
+@pytest.mark.parametrize("cfg,shared,gs", [(SMALL, 0, 64), (SMALL_GQA, 0, 64), ((768, 2048, 12, 12, 12, 32000, 1024),
+                                                                                 0, 64)])
+def test_q8_greedy_matches_runq_oracle(gpu, oracle, cfg, shared, gs):
+    oracle.set_threads(16)
+    c = gpu.Config.make(*cfg)
+    m = gpu.DeviceModel(c, shared, seed=64)
+    q = gpu.DeviceModelQ8(c, shared, gs, from_model=m)
+    state = gpu.DeviceState(c, 1)
+    dec = gpu.Decoder(q, state)
+    dec.set(gpu.OPT_USE_GRAPH, 1)
+    ref = oracle.Model(cfg, shared, seed=64)
+    ref.build_q8(gs)
+    n = 32
+    want = ref.q8_greedy(1, 0, n)
+    got = dec.greedy([1], [0], n)[:, 0].tolist()
+    assert got == want
+    fresh = oracle.Model(cfg, shared, seed=64)
+    fresh.build_q8(gs)
+    for p, t in enumerate([1] + want[:-1]):
+        last = fresh.q8_forward(t, p)
+    assert_ref_close(dec.logits()[0], last, 1e-3, "q8 last-step logits")
+
+
+def test_q8_forward_batch_c_abi(gpu, oracle):
+    cfg = SMALL_GQA
+    c = gpu.Config.make(*cfg)
+    m = gpu.DeviceModel(c, 0, seed=3)
+    q = gpu.DeviceModelQ8(c, 0, 64, from_model=m)
+    B = 3
+    state = gpu.DeviceState(c, B)
+    h = gpu.new_handle()
+    refs = []
+    for _ in range(B):
+        r = oracle.Model(cfg, 0, seed=3)
+        r.build_q8(64)
+        refs.append(r)
+    logits = np.zeros(B * cfg[5], np.float32)
+    toks = np.random.default_rng(1).integers(0, cfg[5], (B, 6))
+    for p in range(6):
+        tk = (C.c_int * B)(*toks[:, p].tolist())
+        ps = (C.c_int * B)(*([p] * B))
+        assert gpu.lib().thaDNN_q8_forward_batch(h, B, C.byref(c), C.byref(q.w), state.ptr, tk, ps,
+                                                 logits.ctypes.data_as(gpu.c_float_p)) == 0
+        for b in range(B):
+            assert_ref_close(logits[b * cfg[5]:(b + 1) * cfg[5]], refs[b].q8_forward(int(toks[b, p]), p), 1e-3,
+                             "q8 abi")
