@@ -164,12 +164,16 @@ TL_DEVICE void row_chunk(const f4* __restrict__ w, const f4* xs, int n4, int cnt
     }
     j = 16;
   }
-  for (; j + 16 <= cnt; j += 16) {
-    f4 wv[16];
+  // 16 wave-loads in flight at one sequence; with several sequences every weight float4
+  // meets NB activation reads, so fewer loads per step keep the registers (and the
+  // occupancy) for the accumulators
+  constexpr int UNR = NB == 1 ? 16 : (NB == 2 ? 8 : 4);
+  for (; j + UNR <= cnt; j += UNR) {
+    f4 wv[UNR];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) wv[u] = load_w4<NT>(w + (j + u) * 64 + lane);
+    for (int u = 0; u < UNR; ++u) wv[u] = load_w4<NT>(w + (j + u) * 64 + lane);
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < UNR; ++u) {
 #pragma unroll
       for (int b = 0; b < NB; ++b) acc[b] = dot4(wv[u], xs[b * n4 + (j + u) * 64 + lane], acc[b]);
     }

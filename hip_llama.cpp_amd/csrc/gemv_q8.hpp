@@ -9,13 +9,16 @@
 // followed by an fp32 scale block [M][K/GS] (runq.c:173-187).
 //
 // Design:
-//  * one wave per row; lane l reads 16 int8 (one dwordx4) of a 1-KiB wave-load,
-//    i.e. a GS=64 group spans 4 lanes; the int8 products use v_dot4_i32_i8
-//    (__builtin_amdgcn_sdot4), the group's int32 sum is completed with two xor
+//  * one wave per row group; lane l reads 16 int8 (one dwordx4) of each 1-KiB
+//    wave-load, so a GS=64 group spans 4 lanes; products use v_dot4_i32_i8
+//    (__builtin_amdgcn_sdot4) and a group's int32 sum is completed with two xor
 //    shuffles and scaled once, exactly like runq's per-group float step;
-//  * the activation quantisation (and the RMSNorm feeding it) is a block prologue:
-//    every block normalises + quantises the activations into LDS (int8 + scales),
-//    so no extra launch and no int8 activation round-trip through HBM.
+//  * a wave keeps IPW items (x2 rows for SwiGLU / QKV pairs) in flight at once:
+//    4 wave-loads per row per step, so 16-32 KiB per wave are outstanding;
+//  * the activation quantisation (and the RMSNorm feeding it) is a cooperative
+//    block prologue: GS/16 threads per group, each normalising and quantising 16
+//    values, a shuffle max per group, one dwordx4 LDS store per thread — no extra
+//    launch and no int8 activation round-trip through HBM.
 #pragma once
 #include "gemv.hpp"
 
@@ -27,45 +30,48 @@ TL_DEVICE int q8_round(float v) {
   return r != r ? 0 : (int)r;
 }
 
-// Stage quantised activations for rows [kc, kc+kcn): xq [NB][kcn] int8, xsc [NB][kcn/gs].
-template <int NB>
+TL_DEVICE f4 rms_apply(f4 v, f4 w, float s) {
+  return f4{__fmul_rn(w.x, __fmul_rn(s, v.x)), __fmul_rn(w.y, __fmul_rn(s, v.y)), __fmul_rn(w.z, __fmul_rn(s, v.z)),
+            __fmul_rn(w.w, __fmul_rn(s, v.w))};
+}
+
+// Quantise activations [kc, kc+kcn) of every live sequence into xq [NB][kcn] int8 and
+// xsc [NB][kcn/gs]; TPG = gs/16 threads per group, 16 values per thread.
+template <int NB, int TPG>
 TL_DEVICE void stage_x_q8(const GemvParams& p, int8_t* xq, float* xsc, int kc, int kcn, const float* ss) {
-  const int gs = p.gs, ng = kcn / gs;
-  for (int e = threadIdx.x; e < NB * ng; e += blockDim.x) {
-    const int b = e / ng, g = e % ng;
-    int8_t* dq = xq + b * kcn + g * gs;
-    if (b >= p.nb) {
-      for (int i = 0; i < gs; i += 4) *reinterpret_cast<int*>(dq + i) = 0;
-      xsc[b * ng + g] = 0.f;
-      continue;
-    }
-    const float* src = p.tok ? p.emb + (long long)p.tok[b] * p.K : p.x + b * p.x_stride;
-    const int k0 = kc + g * gs;
-    // pass 1: max |x'| over the group (x' = RMSNorm output when fused)
-    float wmax = 0.f;
-    for (int i = 0; i < gs; i += 4) {
-      f4 v = *reinterpret_cast<const f4*>(src + k0 + i);
-      if (p.rms_w) {
-        const f4 w = *reinterpret_cast<const f4*>(p.rms_w + k0 + i);
-        v = f4{__fmul_rn(w.x, __fmul_rn(ss[b], v.x)), __fmul_rn(w.y, __fmul_rn(ss[b], v.y)),
-               __fmul_rn(w.z, __fmul_rn(ss[b], v.z)), __fmul_rn(w.w, __fmul_rn(ss[b], v.w))};
+  typedef int i4 __attribute__((ext_vector_type(4)));
+  const int n16 = kcn >> 4;  // 16-value slices per sequence
+  for (int e = threadIdx.x; e < NB * n16; e += blockDim.x) {
+    const int b = e / n16, sl = e % n16;  // TPG consecutive threads own one group
+    const int k0 = kc + sl * 16;
+    f4 v[4];
+    if (b < p.nb) {
+      const float* src = p.tok ? p.emb + (long long)p.tok[b] * p.K : p.x + b * p.x_stride;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[u] = *reinterpret_cast<const f4*>(src + k0 + 4 * u);
+        if (p.rms_w) v[u] = rms_apply(v[u], *reinterpret_cast<const f4*>(p.rms_w + k0 + 4 * u), ss[b]);
       }
-      wmax = fmaxf(wmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = f4{0.f, 0.f, 0.f, 0.f};
     }
-    const float scale = __fdiv_rn(wmax, 127.0f);
-    xsc[b * ng + g] = scale;
-    // pass 2: quantise (x/scale, round half away from zero)
-    for (int i = 0; i < gs; i += 4) {
-      f4 v = *reinterpret_cast<const f4*>(src + k0 + i);
-      if (p.rms_w) {
-        const f4 w = *reinterpret_cast<const f4*>(p.rms_w + k0 + i);
-        v = f4{__fmul_rn(w.x, __fmul_rn(ss[b], v.x)), __fmul_rn(w.y, __fmul_rn(ss[b], v.y)),
-               __fmul_rn(w.z, __fmul_rn(ss[b], v.z)), __fmul_rn(w.w, __fmul_rn(ss[b], v.w))};
-      }
-      const int q0 = q8_round(__fdiv_rn(v.x, scale)), q1 = q8_round(__fdiv_rn(v.y, scale));
-      const int q2 = q8_round(__fdiv_rn(v.z, scale)), q3 = q8_round(__fdiv_rn(v.w, scale));
-      *reinterpret_cast<int*>(dq + i) = (q0 & 0xFF) | ((q1 & 0xFF) << 8) | ((q2 & 0xFF) << 16) | ((q3 & 0xFF) << 24);
+    float m = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+#pragma unroll
+    for (int o = TPG / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    const float scale = __fdiv_rn(m, 127.0f);
+    i4 packed;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q0 = q8_round(__fdiv_rn(v[u].x, scale)), q1 = q8_round(__fdiv_rn(v[u].y, scale));
+      const int q2 = q8_round(__fdiv_rn(v[u].z, scale)), q3 = q8_round(__fdiv_rn(v[u].w, scale));
+      packed[u] = (q0 & 0xFF) | ((q1 & 0xFF) << 8) | ((q2 & 0xFF) << 16) | ((q3 & 0xFF) << 24);
     }
+    *reinterpret_cast<i4*>(xq + b * kcn + sl * 16) = packed;
+    if ((sl % TPG) == 0) xsc[b * (kcn / (TPG * 16)) + sl / TPG] = scale;
   }
 }
 
@@ -92,62 +98,47 @@ TL_DEVICE void q8_item_row(const GemvParams& p, int item, int r, const int8_t*& 
   s = S + row * ng;
 }
 
-// acc[b] += this lane's share of row . xq over [kc, kc + kcn); LPG = lanes per group.
-template <int NB, int LPG, bool NT>
-TL_DEVICE void q8_row_chunk(const int8_t* __restrict__ wq, const float* __restrict__ ws, const int8_t* xq,
-                            const float* xsc, int kc, int kcn, int gs, int lane, float (&acc)[NB]) {
-  typedef int i4 __attribute__((ext_vector_type(4)));
-  const int nfull = kcn >> 10;  // whole 1-KiB wave-loads in the chunk
-  const int gpl = 1024 / gs;    // groups per wave-load
-  const int ng_chunk = kcn / gs;
-  auto step = [&](int j, bool live) {
-    const int kb = j * 1024 + lane * 16;  // byte offset inside the chunk
-    i4 wv = live ? (NT ? __builtin_nontemporal_load(reinterpret_cast<const i4*>(wq + kc + kb))
-                       : *reinterpret_cast<const i4*>(wq + kc + kb))
-                 : i4{0, 0, 0, 0};
-    const int g = j * gpl + lane / LPG;  // group index inside the chunk
-    const float wsc = live ? ws[(kc / gs) + g] : 0.f;
+typedef int q8i4 __attribute__((ext_vector_type(4)));
+
+// One wave-load (16 int8 per lane) of one row against every sequence's activations.
+template <int NB, int LPG>
+TL_DEVICE void q8_dot(q8i4 wv, float wsc, const int8_t* xq, const float* xsc, int kcn, int gidx, int kb, int lane,
+                      float (&acc)[NB]) {
+  const int ng = kcn / (LPG * 16);
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const i4 xv = live ? *reinterpret_cast<const i4*>(xq + b * kcn + kb) : i4{0, 0, 0, 0};
-      int d = __builtin_amdgcn_sdot4(wv.x, xv.x, 0, false);
-      d = __builtin_amdgcn_sdot4(wv.y, xv.y, d, false);
-      d = __builtin_amdgcn_sdot4(wv.z, xv.z, d, false);
-      d = __builtin_amdgcn_sdot4(wv.w, xv.w, d, false);
+  for (int b = 0; b < NB; ++b) {
+    const q8i4 xv = *reinterpret_cast<const q8i4*>(xq + b * kcn + kb);
+    int d = __builtin_amdgcn_sdot4(wv.x, xv.x, 0, false);
+    d = __builtin_amdgcn_sdot4(wv.y, xv.y, d, false);
+    d = __builtin_amdgcn_sdot4(wv.z, xv.z, d, false);
+    d = __builtin_amdgcn_sdot4(wv.w, xv.w, d, false);
 #pragma unroll
-      for (int o = LPG / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
-      if ((lane % LPG) == 0 && live)
-        acc[b] += __fmul_rn(__fmul_rn((float)d, wsc), xsc[b * ng_chunk + (g < ng_chunk ? g : 0)]);
-    }
-  };
-  int j = 0;
-  for (; j + 4 <= nfull; j += 4) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) step(j + u, true);
+    for (int o = LPG / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+    // runq.c:334: val += ((float)ival) * w.s * x.s, once per group (its first lane)
+    if ((lane % LPG) == 0) acc[b] += __fmul_rn(__fmul_rn((float)d, wsc), xsc[b * ng + gidx]);
   }
-  for (; j < nfull; ++j) step(j, true);
-  if (nfull * 1024 < kcn) step(nfull, nfull * 1024 + lane * 16 < kcn);
 }
 
-template <int MODE, int NB, int LPG, bool NT>
-__global__ void __launch_bounds__(256) gemv_q8_kernel(GemvParams p, int kc_max) {
+// WAVES waves, IPW items per wave (RPI rows each) streamed together.
+template <int MODE, int NB, int LPG, bool NT, int WAVES, int IPW>
+__global__ void __launch_bounds__(WAVES * 64) gemv_q8_kernel(GemvParams p, int kc_max) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* red = reinterpret_cast<float*>(smem);  // 16
   float* ss = red + 16;                         // NB (<= 64)
   float* xsc = ss + 64;                         // [NB][kc/gs]
-  int8_t* xq = reinterpret_cast<int8_t*>(xsc + NB * (kc_max / p.gs));  // [NB][kc]
+  int8_t* xq = reinterpret_cast<int8_t*>(xsc + NB * (kc_max / (LPG * 16)));  // [NB][kc]
   constexpr int RPI = RowsPerItem<MODE>::v;
+  constexpr int R = IPW * RPI;  // rows in flight per wave
+  constexpr int GS = LPG * 16;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int item = blockIdx.x * 4 + wave;
-  float acc[RPI][NB];
+  const int item0 = blockIdx.x * (WAVES * IPW) + wave;
+
+  float acc[R][NB];
 #pragma unroll
-  for (int r = 0; r < RPI; ++r)
+  for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[r][b] = 0.f;
-  if (p.rms_w) {
-    rms_scales<NB>(p, ss, red);
-    __syncthreads();
-  }
+  if (p.rms_w) rms_scales<NB>(p, ss, red);
   if (p.tok && blockIdx.x == 0) {  // embedding row -> residual stream (fused lookup)
     for (int e = threadIdx.x; e < p.nb * (p.K / 4); e += blockDim.x) {
       const int b = e / (p.K / 4), j = e % (p.K / 4);
@@ -155,28 +146,67 @@ __global__ void __launch_bounds__(256) gemv_q8_kernel(GemvParams p, int kc_max) 
           reinterpret_cast<const f4*>(p.emb + (long long)p.tok[b] * p.K)[j];
     }
   }
+  // row pointers of this wave's items (rows of dead items point at row 0: loaded, never stored)
+  const int8_t* wq[R];
+  const float* ws[R];
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int item = item0 + i * WAVES;
+#pragma unroll
+    for (int r = 0; r < RPI; ++r) q8_item_row<MODE>(p, item < p.n_items ? item : 0, r, wq[i * RPI + r], ws[i * RPI + r]);
+  }
+
   for (int kc = 0; kc < p.K; kc += kc_max) {
     const int kcn = min(kc_max, p.K - kc);
     if (kc) __syncthreads();
-    stage_x_q8<NB>(p, xq, xsc, kc, kcn, ss);
+    stage_x_q8<NB, LPG>(p, xq, xsc, kc, kcn, ss);
     __syncthreads();
-    if (item < p.n_items) {
+    const int nfull = kcn >> 10;
+    int j = 0;
+    for (; j + 2 <= nfull; j += 2) {  // 2 wave-loads x R rows in flight
+      q8i4 wv[2][R];
+      float sc[2][R];
 #pragma unroll
-      for (int r = 0; r < RPI; ++r) {
-        const int8_t* q;
-        const float* s;
-        q8_item_row<MODE>(p, item, r, q, s);
-        q8_row_chunk<NB, LPG, NT>(q, s, xq, xsc, kc, kcn, p.gs, lane, acc[r]);
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int kb = (j + u) * 1024 + lane * 16;
+          const q8i4* src = reinterpret_cast<const q8i4*>(wq[r] + kc + kb);
+          wv[u][r] = NT ? __builtin_nontemporal_load(src) : *src;
+          sc[u][r] = ws[r][(kc + kb) / GS];
+        }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          q8_dot<NB, LPG>(wv[u][r], sc[u][r], xq, xsc, kcn, ((j + u) * 1024 + lane * 16) / GS, (j + u) * 1024 + lane * 16,
+                          lane, acc[r]);
+    }
+    for (; j * 1024 < kcn; ++j) {  // last full wave-load and/or the partial tail
+      const int kb = j * 1024 + lane * 16;
+      const bool live = kb < kcn;
+      const int kbl = live ? kb : 0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const q8i4* src = reinterpret_cast<const q8i4*>(wq[r] + kc + kbl);
+        q8i4 wv = NT ? __builtin_nontemporal_load(src) : *src;
+        float sc = ws[r][(kc + kbl) / GS];
+        if (!live) { wv = q8i4{0, 0, 0, 0}; sc = 0.f; }
+        q8_dot<NB, LPG>(wv, sc, xq, xsc, kcn, kbl / GS, kbl, lane, acc[r]);
       }
     }
   }
-  if (item >= p.n_items) return;
-  float v[2][NB];
 #pragma unroll
-  for (int r = 0; r < 2; ++r)
+  for (int i = 0; i < IPW; ++i) {
+    const int item = item0 + i * WAVES;
+    if (item >= p.n_items) continue;
+    float v[2][NB];
 #pragma unroll
-    for (int b = 0; b < NB; ++b) v[r][b] = r < RPI ? wave_sum(acc[r < RPI ? r : 0][b]) : 0.f;
-  epilogue<MODE, NB>(p, item, v, lane);
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) v[r][b] = r < RPI ? wave_sum(acc[i * RPI + (r < RPI ? r : 0)][b]) : 0.f;
+    epilogue<MODE, NB>(p, item, v, lane);
+  }
 }
 
 }  // namespace tl

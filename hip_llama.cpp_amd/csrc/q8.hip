@@ -81,11 +81,15 @@ static void launch_q8_one(const GemvParams& p, hipStream_t s, bool nt) {
   if (kc >= p.K) kc = p.K;
   kc -= kc % p.gs;
   const size_t lds = 64 + 256 + (size_t)NB * (kc / p.gs) * 4 + (size_t)NB * kc;
-  const int blocks = (p.n_items + 3) / 4;
+  // items per wave: 4 at one sequence (4-8 rows = 16-32 KiB in flight per wave), 2 above
+  constexpr int IPW = NB == 1 ? 4 : 2;
+  constexpr int WAVES = 4;
+  const int blocks = (p.n_items + WAVES * IPW - 1) / (WAVES * IPW);
   if (nt)
-    hipLaunchKernelGGL((gemv_q8_kernel<MODE, NB, LPG, true>), dim3(blocks), dim3(256), lds, s, p, kc);
+    hipLaunchKernelGGL((gemv_q8_kernel<MODE, NB, LPG, true, WAVES, IPW>), dim3(blocks), dim3(WAVES * 64), lds, s, p, kc);
   else
-    hipLaunchKernelGGL((gemv_q8_kernel<MODE, NB, LPG, false>), dim3(blocks), dim3(256), lds, s, p, kc);
+    hipLaunchKernelGGL((gemv_q8_kernel<MODE, NB, LPG, false, WAVES, IPW>), dim3(blocks), dim3(WAVES * 64), lds, s, p,
+                       kc);
 }
 
 template <int MODE, int NB>
