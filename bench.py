@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-nt", action="store_true")
     ap.add_argument("--splits", type=int, default=0)
+    ap.add_argument("--no-persistent", action="store_true",
+                    help="multi-launch step instead of the one-launch persistent step (batch 1 fp32)")
     ap.add_argument("--cpu-baseline-tokens", type=int, default=2)
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--prof-steps", type=int, default=16)
@@ -130,6 +132,9 @@ def main():
         dec.set(tl.OPT_NT_WEIGHTS, 0)
     if args.splits:
         dec.set(tl.OPT_ATTN_SPLITS, args.splits)
+    if args.no_persistent:
+        dec.set(tl.OPT_PERSISTENT, 0)
+    persistent = dec.persistent()
     log(f"[rank {rank}] {mname} {args.dtype} B={B} init {t_init:.2f}s (broadcast {t_bcast:.2f}s)")
 
     tok0, pos0 = [1] * B, [0] * B  # BOS at position 0
@@ -159,19 +164,32 @@ def main():
 
     # ---------------- per-kernel-class timing: HIP events around every launch on the decoder's
     # stream, over an eager replay of the first prof-steps positions
-    prof = {}
-    if rank == 0:
-        P = min(args.prof_steps, K)
+    # (the persistent step is ONE launch: class "step"; the multi-launch kernels are profiled
+    # as well for the breakdown, with the persistent path switched off)
+    prof, prof_ml = {}, {}
+    P = min(args.prof_steps, K)
+    step_bytes_p = sum(launch_bytes(tl.K_STEP, [p] * B) for p in range(P)) / P
+
+    def profile(into):
         dec.set(tl.OPT_PROFILE, 1)
         dec.prof_reset()
         dec.greedy(tok0, pos0, P, want_tokens=False, sync=True)
         for k, name in enumerate(tl.K_NAMES):
             ms, n = dec.prof(k)
             if n:
-                prof[name] = {"avg_us": 1e3 * ms / n, "launches": n}
-                if k not in (tl.K_ATTN, tl.K_ARGMAX):
-                    prof[name]["GBps"] = launch_bytes(k, [0] * B) / (prof[name]["avg_us"] * 1e-6) / 1e9
+                into[name] = {"avg_us": 1e3 * ms / n, "launches": n}
+                if k == tl.K_STEP:
+                    into[name]["GBps"] = step_bytes_p / (into[name]["avg_us"] * 1e-6) / 1e9
+                elif k not in (tl.K_ATTN, tl.K_ARGMAX):
+                    into[name]["GBps"] = launch_bytes(k, [0] * B) / (into[name]["avg_us"] * 1e-6) / 1e9
         dec.set(tl.OPT_PROFILE, 0)
+
+    if rank == 0:
+        profile(prof)
+        if persistent:
+            dec.set(tl.OPT_PERSISTENT, 0)
+            profile(prof_ml)
+            dec.set(tl.OPT_PERSISTENT, 1)
 
     # ---------------- CPU baseline: the oracle (bit-exact seq.cpp / runq.c restatement), same model
     cpu = None
@@ -202,9 +220,15 @@ def main():
         ref.close()
 
     if rank == 0:
-        ffn = prof.get("ffn_up")
         roof = None
-        if ffn:
+        stp, ffn = prof.get("step"), prof.get("ffn_up")
+        if stp:
+            roof = {"bound": "hbm", "achieved": round(stp["GBps"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(stp["GBps"] / HBM_PEAK_GBS, 4), "traffic": None,
+                    "kernel": "persistent_step_kernel (the whole decode step, one launch)",
+                    "bytes_per_launch": step_bytes_p, "avg_us": round(stp["avg_us"], 2),
+                    "positions": f"0..{P - 1}"}
+        elif ffn:
             roof = {"bound": "hbm", "achieved": round(ffn["GBps"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ffn["GBps"] / HBM_PEAK_GBS, 4), "traffic": None,
                     "kernel": ("gemv_q8_kernel" if q8 else "gemv_kernel") + "<GM_SWIGLU> (RMSNorm + W1/W3 + SwiGLU)",
@@ -220,7 +244,9 @@ def main():
                     "frac_of_peak": round(step_gbs / HBM_PEAK_GBS, 4),
                     "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / step_bytes * B * world, 1)},
             "roofline": roof,
+            "step_path": "persistent" if persistent else "multi-launch",
             "kernels": {k: {kk: round(vv, 2) for kk, vv in v.items()} for k, v in prof.items()},
+            "kernels_multilaunch": {k: {kk: round(vv, 2) for kk, vv in v.items()} for k, v in prof_ml.items()},
             "cpu_baseline": cpu,
             "init_s": round(t_init, 2), "broadcast_s": round(t_bcast, 2),
         }

@@ -135,29 +135,37 @@ struct AttnWaveParams {
   AttnParams a;
   unsigned* cnt;  // [B*H] tickets, zero between launches
   int B, NS;      // NS <= kMaxNS
+  // granule mode (persistent step, B = 1): q and the new K/V row of this step arrive as
+  // tagged granules (common.hpp) from the QKV phase of the same launch; the output leaves
+  // as granules for the Wo phase
+  const unsigned long long* gqkv;  // [dim + 2*kv_dim]: q | k_new | v_new
+  unsigned long long* gout;        // [dim]
+  unsigned tag_in, tag_out;
+  unsigned* err;
 };
 
-TL_DEVICE void st_sc1(float* p, float v) {
-  __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-TL_DEVICE float ld_sc1(const float* p) {
-  return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT));
-}
+TL_DEVICE void st_sc1(float* p, float v) { st1_sc1(p, v); }
+TL_DEVICE float ld_sc1(const float* p) { return ld1_sc1(p); }
 
-template <int HS, int CH>
-__global__ void __launch_bounds__(64) attn_wave_kernel(AttnWaveParams w) {
+// Orders one wave's LDS strip writes before its reads (and vice versa): LDS ops of a
+// wave retire in order, this only stops the compiler from moving them.
+TL_DEVICE void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// The body of one attention unit, run by one full wave.  `sc` is this wave's private
+// 64-float LDS strip; `unit` must be wave-uniform.  Also used inside the persistent step
+// kernel (persist.hip) with GR = true: q and the K/V rows at position pos come from the
+// granules the QKV phase of the same launch published (rows < pos were written by earlier
+// launches and are read from the cache), and the output is published as granules.
+template <int HS, int CH, bool GR = false>
+TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane) {
   constexpr int LPK = HS / 4;    // lanes per key row (one float4 each)
   constexpr int KPI = 64 / LPK;  // keys per wave-instruction
   constexpr int NI = CH / KPI;   // K wave-loads per chunk
   constexpr int VPL = HS / 64;   // output columns per lane
   static_assert(CH <= 64 && HS % 64 == 0, "chunk <= 64 keys, head size multiple of 64");
-  __shared__ float sc[64];
   const AttnParams& p = w.a;
-  const int lane = threadIdx.x;
   const int BH = w.B * p.n_heads;
-  const int s = blockIdx.x / BH, bh = blockIdx.x % BH;
+  const int s = unit / BH, bh = unit % BH;
   const int b = bh / p.n_heads, h = bh % p.n_heads;
   const int T = p.pos[b] + 1;
   const int nchunks = (T + CH - 1) / CH;
@@ -167,7 +175,14 @@ __global__ void __launch_bounds__(64) attn_wave_kernel(AttnWaveParams w) {
   const int kvh = h / p.kv_mul;
   const float* kbase = p.kc + (long long)b * p.kv_b_stride + p.kv_l_off + (long long)kvh * HS;
   const float* vbase = p.vc + (long long)b * p.kv_b_stride + p.kv_l_off + (long long)kvh * HS;
-  const f4 qv = reinterpret_cast<const f4*>(p.q + (long long)b * p.dim + h * HS)[lane % LPK];
+  const float* qrow = p.q + (long long)b * p.dim + h * HS;
+  f4 qv;
+  // granule mode: q and the new key / value row (position T-1) are waited for only after the
+  // first chunk's cached rows are in flight
+  __amdgpu_buffer_rsrc_t rg;
+  bool qready = false;
+  if constexpr (GR) rg = rsrc_of(w.gqkv);
+  else qv = reinterpret_cast<const f4*>(qrow)[lane % LPK];
   const float rs = sqrtf((float)HS);
   const bool whole = nchunks == 1;
 
@@ -182,16 +197,53 @@ __global__ void __launch_bounds__(64) attn_wave_kernel(AttnWaveParams w) {
     // clamped to its last row: loaded, weighted by 0)
     f4 kv[NI];
     float vv[CH][VPL];
+    if constexpr (GR) {
+      // rows already in the cache (t < T-1) first; the row this step writes (t = T-1) is
+      // patched in from the granules once they are published
+      const int tc = T >= 2 ? T - 2 : 0;
 #pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int t = min(t0 + i * KPI + lane / LPK, t1 - 1);
-      kv[i] = reinterpret_cast<const f4*>(kbase + (long long)t * p.kv_dim)[lane % LPK];
-    }
+      for (int i = 0; i < NI; ++i) {
+        const int t = min(min(t0 + i * KPI + lane / LPK, t1 - 1), tc);
+        kv[i] = reinterpret_cast<const f4*>(kbase + (long long)t * p.kv_dim)[lane % LPK];
+      }
 #pragma unroll
-    for (int u = 0; u < CH; ++u) {
-      const float* vr = vbase + (long long)min(t0 + u, t1 - 1) * p.kv_dim + lane * VPL;
+      for (int u = 0; u < CH; ++u) {
+        const float* vr = vbase + (long long)min(min(t0 + u, t1 - 1), tc) * p.kv_dim + lane * VPL;
 #pragma unroll
-      for (int c = 0; c < VPL; ++c) vv[u][c] = vr[c];
+        for (int c = 0; c < VPL; ++c) vv[u][c] = vr[c];
+      }
+      if (!qready) {
+        qv = gran_wait4(rg, (unsigned)(h * HS + (lane % LPK) * 4) * 8u, w.tag_in, w.err);
+        qready = true;
+      }
+      if (t1 == T) {  // this chunk holds the new row
+        const unsigned kofs = (unsigned)(p.dim + kvh * HS), vofs = (unsigned)(p.dim + p.kv_dim + kvh * HS);
+        const f4 kn = gran_wait4(rg, (kofs + (lane % LPK) * 4) * 8u, w.tag_in, w.err);
+        float vn[VPL];
+#pragma unroll
+        for (int c = 0; c < VPL; ++c) vn[c] = gran_wait(w.gqkv + vofs + lane * VPL + c, w.tag_in, w.err);
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+          if (min(t0 + i * KPI + lane / LPK, t1 - 1) == T - 1) kv[i] = kn;
+#pragma unroll
+        for (int u = 0; u < CH; ++u)
+          if (min(t0 + u, t1 - 1) == T - 1) {
+#pragma unroll
+            for (int c = 0; c < VPL; ++c) vv[u][c] = vn[c];
+          }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int t = min(t0 + i * KPI + lane / LPK, t1 - 1);
+        kv[i] = reinterpret_cast<const f4*>(kbase + (long long)t * p.kv_dim)[lane % LPK];
+      }
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const float* vr = vbase + (long long)min(t0 + u, t1 - 1) * p.kv_dim + lane * VPL;
+#pragma unroll
+        for (int c = 0; c < VPL; ++c) vv[u][c] = vr[c];
+      }
     }
     // scores (reference src/seq.cpp:107-117)
 #pragma unroll
@@ -200,9 +252,9 @@ __global__ void __launch_bounds__(64) attn_wave_kernel(AttnWaveParams w) {
       const int t = i * KPI + lane / LPK;
       if ((lane % LPK) == 0 && t < n) sc[t] = __fdiv_rn(d, rs);
     }
-    __syncthreads();  // one-wave block: orders the score strip
+    wave_lds_fence();  // score strip written
     const float my = lane < n ? sc[lane] : -3.402823466e+38f;
-    __syncthreads();  // the strip is rewritten by the next chunk
+    wave_lds_fence();  // the strip is rewritten by the next chunk
     const float mc = wave_max(my);
     float pr;
     if (whole) {
@@ -230,8 +282,13 @@ __global__ void __launch_bounds__(64) attn_wave_kernel(AttnWaveParams w) {
 
   float* out = p.out + (long long)b * p.dim + h * HS + lane * VPL;
   if (whole) {
+    if constexpr (GR) {
 #pragma unroll
-    for (int c = 0; c < VPL; ++c) out[c] = o[c];
+      for (int c = 0; c < VPL; ++c) st8_sc1(w.gout + h * HS + lane * VPL + c, gran(w.tag_out, o[c]));
+    } else {
+#pragma unroll
+      for (int c = 0; c < VPL; ++c) out[c] = o[c];
+    }
     return;
   }
   // publish this unit's partial (write-through), drain, take a ticket
@@ -275,12 +332,26 @@ __global__ void __launch_bounds__(64) attn_wave_kernel(AttnWaveParams w) {
     for (int c = 0; c < VPL; ++c) acc[c] = fmaf(ov[k][c], a, acc[c]);
   }
 #pragma unroll
-  for (int c = 0; c < VPL; ++c) out[c] = __fdiv_rn(acc[c], L);
+  for (int c = 0; c < VPL; ++c) acc[c] = __fdiv_rn(acc[c], L);
+  if constexpr (GR) {
+#pragma unroll
+    for (int c = 0; c < VPL; ++c) st8_sc1(w.gout + h * HS + lane * VPL + c, gran(w.tag_out, acc[c]));
+  } else {
+#pragma unroll
+    for (int c = 0; c < VPL; ++c) out[c] = acc[c];
+  }
   if (lane == 0) __hip_atomic_store(w.cnt + bh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Stand-alone launch: one 64-thread block per unit.
+template <int HS, int CH>
+__global__ void __launch_bounds__(64) attn_wave_kernel(AttnWaveParams w) {
+  __shared__ float sc[64];
+  attn_unit<HS, CH>(w, blockIdx.x, sc, threadIdx.x);
+}
+
 // out[b][h*hs + i] = sum_s o_s[i] e^{m_s-M} / sum_s l_s e^{m_s-M}
-__global__ void __launch_bounds__(256) attn_combine_kernel(AttnParams p) {
+static __global__ void __launch_bounds__(256) attn_combine_kernel(AttnParams p) {
   const int h = blockIdx.x, b = blockIdx.y;
   const int hs = p.head_size;
   const int T = p.pos[b] + 1;

@@ -30,6 +30,7 @@
 #include "attention.hpp"
 #include "gemv_dispatch.hpp"
 #include "q8_dispatch.hpp"
+#include "persist.hpp"
 
 using tl::f4;
 
@@ -129,7 +130,18 @@ struct thallama_decoder {
   bool nt = true;
   bool use_graph = false;
   bool profile = false;
+  bool persist = true;          // requested (THALLAMA_OPT_PERSISTENT)
   hipGraphExec_t exec = nullptr;
+  // persistent one-launch step (persist.hip)
+  int ncu = 0;
+  unsigned* psync = nullptr;    // [kPSyncWords shards][L*H tickets] (zeroed per launch), err, seq
+  size_t psync_zero = 0;        // words zeroed before every launch
+  unsigned long long* pbmax = nullptr;
+  unsigned long long* pgran = nullptr;  // hand-off granules: x | xb | hb | qkv
+  bool pok = false;             // shape supported
+  unsigned long long* ptrace = nullptr;  // optional timeline of the persistent step
+  size_t ptrace_n = 0;
+  std::string pwhy;             // why not
   // profiling
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, int>> ev_marks;  // (class, event index of start)
@@ -245,6 +257,26 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
   const double wbytes = 4.0 * ((double)d->L * (2.0 * d->dim * d->dim + 2.0 * d->dim * d->kv_dim +
                                                3.0 * d->dim * d->hidden) + (double)d->V * d->dim);
   d->nt = wbytes > 1024.0 * 1024.0 * 1024.0;
+  // persistent step: batch 1, fp32 (decided again for int8 in _create_q8)
+  TL_TRY(hipDeviceGetAttribute(&d->ncu, hipDeviceAttributeMultiprocessorCount, d->dev));
+  if (batch == 1) {
+    tl::PStep ps = {};
+    ps.dim = d->dim; ps.hid = d->hidden; ps.kvd = d->kv_dim; ps.hs = d->hs; ps.NS = d->nsplit;
+    const char* why = nullptr;
+    d->pok = tl::persistent_prepare(ps, d->ncu, &why);
+    if (!d->pok && why) d->pwhy = why;
+  } else {
+    d->pwhy = "batch > 1";
+  }
+  if (d->pok) {
+    d->psync_zero = tl::kPSyncWords + (((size_t)d->L * d->H + 3) & ~(size_t)3);
+    TL_TRY(hipMalloc(&d->psync, sizeof(unsigned) * (d->psync_zero + 32)));
+    TL_TRY(hipMemset(d->psync, 0, sizeof(unsigned) * (d->psync_zero + 32)));
+    TL_TRY(hipMalloc(&d->pbmax, sizeof(unsigned long long) * d->ncu));
+    const size_t ng = (size_t)3 * d->dim + d->hidden + 2 * d->kv_dim;
+    TL_TRY(hipMalloc(&d->pgran, sizeof(unsigned long long) * ng));
+    TL_TRY(hipMemset(d->pgran, 0, sizeof(unsigned long long) * ng));
+  }
   *out = d;
   return 0;
 }
@@ -262,6 +294,10 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   (void)hipFree(d->rope_d);
   (void)hipFree(d->part_d);
   (void)hipFree(d->cnt_d);
+  (void)hipFree(d->psync);
+  (void)hipFree(d->pbmax);
+  (void)hipFree(d->pgran);
+  (void)hipFree(d->ptrace);
   if (d->own_stream) (void)hipStreamDestroy(d->stream);
   delete d;
 }
@@ -273,6 +309,7 @@ extern "C" int thallama_decoder_set(thallama_decoder* d, int key, int value) {
     case THALLAMA_OPT_ATTN_SPLITS: d->nsplit = value <= 0 ? auto_splits(d) : (value > 16 ? 16 : value); break;
     case THALLAMA_OPT_USE_GRAPH: d->use_graph = value != 0; break;
     case THALLAMA_OPT_PROFILE: d->profile = value != 0; break;
+    case THALLAMA_OPT_PERSISTENT: d->persist = value != 0; break;
     default: return (int)hipErrorInvalidValue;
   }
   if (d->exec) {  // options are baked into a captured graph: recapture on next use
@@ -472,6 +509,74 @@ static int enqueue_step(thallama_decoder* d) {
   return 0;
 }
 
+static bool use_persist(const thallama_decoder* d) { return d->persist && d->pok && !d->q8; }
+
+// The whole step (and, for greedy decoding, the argmax + advance) as one persistent launch.
+static int enqueue_persistent(thallama_decoder* d, bool argmax) {
+  const TransformerWeights& w = d->w;
+  const RunState& s = d->s;
+  tl::PStep p = {};
+  p.emb = w.token_embedding_table; p.rms_att = w.rms_att_weight; p.rms_ffn = w.rms_ffn_weight;
+  p.wq = w.wq; p.wk = w.wk; p.wv = w.wv; p.wo = w.wo; p.w1 = w.w1; p.w2 = w.w2; p.w3 = w.w3;
+  p.rms_final = w.rms_final_weight; p.wcls = w.wcls;
+  p.dim = d->dim; p.hid = d->hidden; p.kvd = d->kv_dim; p.L = d->L; p.S = d->S; p.V = d->V; p.H = d->H;
+  p.kv_mul = d->kv_mul; p.hs = d->hs; p.NS = d->nsplit;
+  p.x = s.x; p.xb = s.xb; p.logits = s.logits; p.kc = s.key_cache; p.vc = s.value_cache;
+  p.part = d->part_d; p.rope = d->rope_d;
+  p.tok = d->tok_d; p.pos = d->pos_d; p.out = d->out_d;
+  p.gx = d->pgran; p.gxb = p.gx + d->dim; p.ghb = p.gxb + d->dim; p.gqkv = p.ghb + d->hidden;
+  p.sync = d->psync; p.tickets = d->psync + tl::kPSyncWords;
+  p.err = d->psync + d->psync_zero; p.seq = p.err + 1; p.bmax = d->pbmax;
+  p.argmax = argmax ? 1 : 0;
+  p.trace = d->ptrace;
+  const char* why = nullptr;
+  if (!tl::persistent_prepare(p, d->ncu, &why)) {
+    g_last_error = std::string("persistent step: ") + (why ? why : "unsupported");
+    return (int)hipErrorInvalidValue;
+  }
+  TL_TRY(hipMemsetAsync(p.sync, 0, sizeof(unsigned) * d->psync_zero, d->stream));
+  const int ev = prof_begin(d);
+  TL_TRY(tl::launch_persistent_step(p, d->stream, d->ncu));
+  prof_end(d, THALLAMA_K_STEP, ev);
+  return 0;
+}
+
+// After a synchronisation: did a persistent grid barrier give up?  (Only possible if the
+// grid was not co-resident; the step's results are then wrong and the path is disabled.)
+static int check_persist(thallama_decoder* d) {
+  if (!d->psync) return 0;
+  unsigned err = 0;
+  TL_TRY(hipMemcpy(&err, d->psync + d->psync_zero, sizeof(unsigned), hipMemcpyDeviceToHost));
+  if (!err) return 0;
+  TL_TRY(hipMemset(d->psync, 0, sizeof(unsigned) * (d->psync_zero + 32)));
+  TL_TRY(hipMemset(d->cnt_d, 0, sizeof(unsigned) * (size_t)d->B * d->H));
+  d->pok = false;
+  d->pwhy = "a grid barrier timed out";
+  g_last_error = "persistent step: a grid barrier timed out (grid not co-resident); path disabled";
+  return (int)hipErrorLaunchFailure;
+}
+
+extern "C" int thallama_decoder_persistent(thallama_decoder* d) { return d && use_persist(d) ? 1 : 0; }
+
+// Timeline of the persistent step (tools/persist_trace.py): enable allocates the buffer;
+// every later launch overwrites it; copy returns [grid][5L+1][4] 100-MHz stamps.
+extern "C" int thallama_decoder_ptrace(thallama_decoder* d, int enable, unsigned long long* host, size_t n) {
+  if (!d) return (int)hipErrorInvalidValue;
+  const size_t need = (size_t)d->ncu * (5 * d->L + 1) * 4;
+  if (enable && !d->ptrace) {
+    TL_TRY(hipMalloc(&d->ptrace, need * sizeof(unsigned long long)));
+    TL_TRY(hipMemset(d->ptrace, 0, need * sizeof(unsigned long long)));
+    d->ptrace_n = need;
+    if (d->exec) { (void)hipGraphExecDestroy(d->exec); d->exec = nullptr; }
+  }
+  if (host && d->ptrace) {
+    TL_TRY(hipStreamSynchronize(d->stream));
+    TL_TRY(hipMemcpy(host, d->ptrace, (n < d->ptrace_n ? n : d->ptrace_n) * sizeof(unsigned long long),
+                     hipMemcpyDeviceToHost));
+  }
+  return (int)need;
+}
+
 static int enqueue_argmax(thallama_decoder* d) {
   int ev = prof_begin(d);
   hipLaunchKernelGGL(k_argmax_advance, dim3(d->B), dim3(1024), 0, d->stream, d->s.logits, d->V, d->tok_d,
@@ -501,14 +606,14 @@ extern "C" int thallama_decoder_forward(thallama_decoder* d, const int* token_h,
   if (!d || !token_h || !pos_h) return (int)hipErrorInvalidValue;
   int r = upload_tok_pos(d, token_h, pos_h);
   if (r) return r;
-  r = enqueue_step(d);
+  r = use_persist(d) ? enqueue_persistent(d, false) : enqueue_step(d);
   if (r) return r;
   if (logits_h)
     TL_TRY(hipMemcpyAsync(logits_h, d->s.logits, sizeof(float) * (size_t)d->B * d->V, hipMemcpyDeviceToHost,
                           d->stream));
   TL_TRY(hipStreamSynchronize(d->stream));
   prof_collect(d);
-  return 0;
+  return check_persist(d);
 }
 
 extern "C" int thallama_decoder_greedy(thallama_decoder* d, const int* token0_h, const int* pos0_h, int n_steps,
@@ -525,8 +630,13 @@ extern "C" int thallama_decoder_greedy(thallama_decoder* d, const int* token0_h,
   if (graph && !d->exec) {
     hipGraph_t g = nullptr;
     TL_TRY(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
-    int e = enqueue_step(d);
-    if (!e) e = enqueue_argmax(d);
+    int e = 0;
+    if (use_persist(d)) {
+      e = enqueue_persistent(d, true);
+    } else {
+      e = enqueue_step(d);
+      if (!e) e = enqueue_argmax(d);
+    }
     hipError_t ce = hipStreamEndCapture(d->stream, &g);
     if (e) return e;
     TL_TRY(ce);
@@ -536,6 +646,9 @@ extern "C" int thallama_decoder_greedy(thallama_decoder* d, const int* token0_h,
   for (int i = 0; i < n_steps; ++i) {
     if (graph) {
       TL_TRY(hipGraphLaunch(d->exec, d->stream));
+    } else if (use_persist(d)) {
+      r = enqueue_persistent(d, true);
+      if (r) return r;
     } else {
       r = enqueue_step(d);
       if (r) return r;
@@ -552,9 +665,12 @@ extern "C" int thallama_decoder_greedy(thallama_decoder* d, const int* token0_h,
       for (int b = 0; b < d->B; ++b) tokens_out_h[(size_t)i * d->B + b] = tmp[(size_t)b * d->S + pos0_h[b] + i];
   } else if (sync) {
     TL_TRY(hipStreamSynchronize(d->stream));
+  } else {
+    prof_collect(d);
+    return 0;
   }
   prof_collect(d);
-  return 0;
+  return check_persist(d);
 }
 
 extern "C" int thallama_decoder_logits(thallama_decoder* d, float* logits_h) {
@@ -597,6 +713,11 @@ extern "C" double thallama_step_bytes(const Config* c, int B, int kclass, const 
     case THALLAMA_K_FFN_DOWN: return 4.0 * (hid * dim + B * (hid + 2 * dim));
     case THALLAMA_K_CLS: return 4.0 * (V * dim + dim + B * (dim + V));
     case THALLAMA_K_ARGMAX: return 4.0 * B * V;
+    case THALLAMA_K_STEP: {
+      double t = 0;
+      for (int k = THALLAMA_K_QKV; k <= THALLAMA_K_FFN_DOWN; ++k) t += c->n_layers * thallama_step_bytes(c, B, k, pos_h);
+      return t + thallama_step_bytes(c, B, THALLAMA_K_CLS, pos_h) + thallama_step_bytes(c, B, THALLAMA_K_ARGMAX, pos_h);
+    }
   }
   return 0;
 }

@@ -1,0 +1,522 @@
+// persist.hip — the whole batch-1 fp32 decode step as ONE persistent launch.
+//
+// Semantics: the reference forward (src/seq.cpp:53-168; GPU twin src/thaDNN.cpp:13-260)
+// followed, in greedy mode, by sample_argmax (src/llama.cpp:275-286).
+//
+// Why one launch: every launch of the streaming GEMV pays a fixed ~4 us (first-byte HBM
+// latency, tail, boundary; fitted over profiles/r01_gemv_sweep.json: t = bytes / ~7 TB/s +
+// ~4.2 us), and the multi-launch step (forward.hip) has 5 launches per layer.
+//
+// Structure: grid = one 576-thread block (9 waves) per CU, all co-resident.  Phases per layer:
+// QKV (+RMSNorm, RoPE, KV write) | attention | Wo + residual | W1/W3 + RMSNorm + SwiGLU |
+// W2 + residual; then the classifier (+RMSNorm) and the argmax.  Per phase a block owns a
+// contiguous range of items (rows, or row pairs for QKV / SwiGLU); their 8-KiB row chunks
+// ("slots") are dealt round-robin to the 8 streaming waves, which keep two slots in flight
+// and, as soon as they finish a phase, issue their first two slots of the NEXT phase.
+// Wave 0 is the control wave: epilogues, attention units, norm-weight preloads.
+//
+// Hand-offs between phases carry their own readiness (MI355X_MICROARCH.md § visibility, R2
+// granules): every float another block needs (x, q / k_new / v_new, the attention output,
+// hb) is published as an 8-byte {value, tag} granule with one sc1 store, and the consumer
+// (the next phase's staging, or an attention unit) re-reads until the tag matches.  No grid
+// barrier, fence, drain or flag between phases: a phase starts as soon as ITS inputs exist.
+// Tags are (launch sequence << 12) + phase + 1 — unique between consecutive launches, with
+// the sequence word kept in device memory (advanced by block 0 after the final barrier), so
+// granule buffers never need clearing and graph replays stay correct.  The only grid barrier
+// is the final one (per-block argmax winners -> block 0).  Every wait is bounded and sets a
+// sticky error word the host checks (a grid that is not co-resident cannot hang the GPU).
+//
+// Why hand-offs are safe to overwrite (write-after-read): a buffer is rewritten only by a
+// phase whose inputs transitively required EVERY block to finish the phase that read it
+// (e.g. x is rewritten by W2(l) only after every block published hb(l), i.e. finished
+// staging x for W1/W3(l)); see DESIGN.md.
+#include <hip/hip_runtime.h>
+#include "attention.hpp"
+#include "gemv.hpp"
+#include "persist.hpp"
+
+namespace tl {
+
+constexpr int PW = 9;        // waves per block: 1 control + 8 streaming
+constexpr int PT = PW * 64;  // threads per block
+constexpr int PL = 8;        // wave-loads per slot (8 KiB per wave)
+constexpr int NSW = PW - 1;  // streaming waves per block
+constexpr int SB = 4;        // staged float4 per thread and batch (granule loads in flight)
+constexpr int kPResidFloats = 256;  // residual-stream slice per block (LDS)
+constexpr unsigned kSpinLimit = 1u << 18;
+
+enum PKind : int { PK_QKV = 0, PK_ATTN = 1, PK_WO = 2, PK_UP = 3, PK_DOWN = 4, PK_CLS = 5 };
+
+// One GEMV phase, described at run time (a single copy of the streaming loop serves every
+// phase, so the compiler has nothing per phase to hoist and keep live across the step).
+struct PDesc {
+  int kind;                      // PKind (never PK_ATTN)
+  int K;                         // row length (floats)
+  int n_items;                   // rows, or row pairs (QKV, SwiGLU)
+  int rpi;                       // rows per item
+  const float* W0;               // QKV: Wq | W1 (SwiGLU) | W
+  const float* W1;               // QKV: Wk | W3
+  const float* W2;               // QKV: Wv
+  const unsigned long long* gin; // input granules (null: the token's embedding row)
+  unsigned tag_in;
+  const float* rms;              // fused RMSNorm weight or null
+  unsigned long long* gout;      // output granules (null for the classifier)
+  unsigned tag_out;
+};
+
+TL_DEVICE PDesc make_desc(const PStep& p, int kind, int l, unsigned tb) {
+  PDesc d = {};
+  d.kind = kind;
+  const long long ll = l, dim = p.dim, hid = p.hid, kvd = p.kvd;
+  const unsigned t0 = tb + 5u * l;  // tag of the phase before QKV(l), i.e. W2(l-1)
+  switch (kind) {
+    case PK_QKV:
+      d.K = p.dim; d.n_items = (p.dim + 2 * p.kvd) / 2; d.rpi = 2;
+      d.W0 = p.wq + ll * dim * dim; d.W1 = p.wk + ll * dim * kvd; d.W2 = p.wv + ll * dim * kvd;
+      d.gin = l == 0 ? nullptr : p.gx; d.tag_in = t0;
+      d.rms = p.rms_att + ll * dim; d.gout = p.gqkv; d.tag_out = t0 + 1;
+      break;
+    case PK_WO:
+      d.K = p.dim; d.n_items = p.dim; d.rpi = 1;
+      d.W0 = p.wo + ll * dim * dim; d.gin = p.gxb; d.tag_in = t0 + 2; d.gout = p.gx; d.tag_out = t0 + 3;
+      break;
+    case PK_UP:
+      d.K = p.dim; d.n_items = p.hid; d.rpi = 2;
+      d.W0 = p.w1 + ll * dim * hid; d.W1 = p.w3 + ll * dim * hid;
+      d.gin = p.gx; d.tag_in = t0 + 3; d.rms = p.rms_ffn + ll * dim; d.gout = p.ghb; d.tag_out = t0 + 4;
+      break;
+    case PK_DOWN:
+      d.K = p.hid; d.n_items = p.dim; d.rpi = 1;
+      d.W0 = p.w2 + ll * dim * hid; d.gin = p.ghb; d.tag_in = t0 + 4; d.gout = p.gx; d.tag_out = t0 + 5;
+      break;
+    default:  // PK_CLS (l = L)
+      d.K = p.dim; d.n_items = p.V; d.rpi = 1;
+      d.W0 = p.wcls; d.gin = p.L == 0 ? nullptr : p.gx; d.tag_in = tb + 5u * p.L; d.rms = p.rms_final;
+      break;
+  }
+  return d;
+}
+
+// The GEMV phase that follows `kind` at layer l (attention has no weights).
+TL_DEVICE PDesc next_desc(const PStep& p, int kind, int l, unsigned tb) {
+  if (kind == PK_QKV) return make_desc(p, PK_WO, l, tb);
+  if (kind == PK_WO) return make_desc(p, PK_UP, l, tb);
+  if (kind == PK_UP) return make_desc(p, PK_DOWN, l, tb);
+  return l + 1 < p.L ? make_desc(p, PK_QKV, l + 1, tb) : make_desc(p, PK_CLS, p.L, tb);
+}
+
+// Geometry of a phase for this block (all wave-uniform).  A slot is one 8-KiB chunk of one
+// row: row rl of the block, floats [c*2048, c*2048 + 2048).
+struct PGeo {
+  int rowb;  // row length in bytes
+  int nch;   // chunks per row
+  int i0;    // first item of this block
+  int ni;    // items of this block
+  int nslot; // slots of this block (ni * rpi * nch)
+};
+
+TL_DEVICE PGeo geo(const PDesc& d) {
+  PGeo g;
+  g.rowb = d.K * 4;
+  g.nch = (d.K + PL * 256 - 1) / (PL * 256);
+  const long long G = gridDim.x, bi = blockIdx.x;
+  g.i0 = (int)(bi * d.n_items / G);
+  g.ni = (int)((bi + 1) * d.n_items / G) - g.i0;
+  g.nslot = g.ni * d.rpi * g.nch;
+  return g;
+}
+
+// Weight row R (global row index within the phase's matrix set).
+TL_DEVICE const float* row_ptr(const PDesc& d, const PStep& p, int R) {
+  const long long K = d.K;
+  if (d.kind == PK_UP) return ((R & 1) ? d.W1 : d.W0) + (long long)(R >> 1) * K;
+  if (d.kind == PK_QKV) {
+    if (R < p.dim) return d.W0 + (long long)R * K;
+    R -= p.dim;
+    if (R < p.kvd) return d.W1 + (long long)R * K;
+    return d.W2 + (long long)(R - p.kvd) * K;
+  }
+  return d.W0 + (long long)R * K;
+}
+
+// Issue the 8 wave-loads of `slot` into buf: raw buffer loads over one row (the resource's
+// size is what is left of the row, so loads past its end return 0 without touching memory,
+// and a slot past the block's end is a zero-size resource: every slot is exactly PL loads
+// and the compiler's vmcnt bookkeeping stays exact — A/B double buffer, vmcnt(PL)).
+TL_DEVICE void load_slot(const PDesc& d, const PGeo& g, const PStep& p, int slot, int lane, f4 (&buf)[PL]) {
+  const bool sv = slot < g.nslot;
+  const int rl = slot / g.nch, c = slot - rl * g.nch;
+  const float* row = sv ? row_ptr(d, p, g.i0 * d.rpi + rl) : d.W0;
+  // one resource per 4 KiB quarter, so the per-load offsets fit the 12-bit immediate
+#pragma unroll
+  for (int q = 0; q < PL / 4; ++q) {
+    const int off = c * (PL * 1024) + q * 4096;  // bytes into the row
+    const int left = sv ? g.rowb - off : 0;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(row) + off / 4, (short)0,
+                                                      left > 0 ? left : 0, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      buf[q * 4 + u] =
+          __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16 + u * 1024, 0, 2 /*nt*/));
+  }
+}
+
+TL_DEVICE void consume_slot(const PGeo& g, int slot, int lane, const f4 (&buf)[PL], const f4* xs, float* res) {
+  const int c = slot % g.nch;
+  const f4* xc = xs + c * (PL * 64) + lane;
+  float a = 0.f;
+  // four LDS reads in flight at a time: the activations must not need a third register set
+#pragma unroll
+  for (int q = 0; q < PL / 4; ++q) {
+#pragma unroll
+    for (int u = q * 4; u < q * 4 + 4; ++u) a = dot4(buf[u], xc[u * 64], a);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  a = wave_sum(a);
+  if (lane == 0) res[slot] = a;
+}
+
+// Stream this wave's slots (sw, sw + NSW, ...), sw = streaming-wave index; A/B already hold
+// the first two.  Every path loads A and B in the same two places, so the register
+// allocator keeps one pair of register sets for the whole step.
+TL_DEVICE void run_gemv(const PDesc& d, const PGeo& g, const PStep& p, int sw, int lane, const f4* xs,
+                        float* res, f4 (&A)[PL], f4 (&B)[PL]) {
+  const int nk = g.nslot > sw ? (g.nslot - sw + NSW - 1) / NSW : 0;
+  // sched_barrier: keep each refill behind the slot's last use (no third register set)
+  for (int k = 0; k < nk; k += 2) {
+    consume_slot(g, sw + k * NSW, lane, A, xs, res);
+    __builtin_amdgcn_sched_barrier(0);
+    load_slot(d, g, p, sw + (k + 2) * NSW, lane, A);
+    __builtin_amdgcn_sched_barrier(0);
+    if (k + 1 < nk) consume_slot(g, sw + (k + 1) * NSW, lane, B, xs, res);
+    __builtin_amdgcn_sched_barrier(0);
+    load_slot(d, g, p, sw + (k + 3) * NSW, lane, B);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Every wave stages the phase input into LDS (zero-padded to whole chunks), RMSNorm'd when
+// the phase has a norm (its weights were preloaded into LDS `rmsw` by the control wave).
+// The input is the previous phase's granules (all issued at once, then re-polled until
+// their tags match), or — QKV at layer 0, or the classifier of a model without layers —
+// the token's embedding row (weights: plain loads).  Ends with a workgroup barrier.
+TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, const float* rmsw, float* red,
+                     int wave, int lane) {
+  const int n4 = d.K >> 2, pad4 = g.nch * PL * 64;
+  float sq = 0.f;
+  if (!d.gin) {
+    const f4* emb = reinterpret_cast<const f4*>(p.emb + (long long)p.tok[0] * p.dim);
+    for (int j = threadIdx.x; j < pad4; j += PT) {
+      const f4 v = j < n4 ? emb[j] : f4{0.f, 0.f, 0.f, 0.f};
+      sq = fmaf(v.x, v.x, sq); sq = fmaf(v.y, v.y, sq); sq = fmaf(v.z, v.z, sq); sq = fmaf(v.w, v.w, sq);
+      xs[j] = v;
+    }
+  } else {
+    const auto r = rsrc_of(d.gin);
+    // batches of SB float4 (2*SB loads in flight per thread), then re-poll what was late
+    for (int k0 = 0; k0 * PT < pad4; k0 += SB) {
+      v4u a[SB], b[SB];
+#pragma unroll
+      for (int k = 0; k < SB; ++k) {
+        const int j = threadIdx.x + (k0 + k) * PT;
+        if (j < n4) {
+          a[k] = ld16_sc1(r, (unsigned)j * 32u);
+          b[k] = ld16_sc1(r, (unsigned)j * 32u + 16u);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < SB; ++k) {
+        const int j = threadIdx.x + (k0 + k) * PT;
+        if (j < pad4) {
+          f4 v = f4{0.f, 0.f, 0.f, 0.f};
+          if (j < n4)
+            v = gran4_ok(a[k], b[k], d.tag_in) ? gran4_val(a[k], b[k])
+                                               : gran_wait4(r, (unsigned)j * 32u, d.tag_in, p.err);
+          sq = fmaf(v.x, v.x, sq); sq = fmaf(v.y, v.y, sq); sq = fmaf(v.z, v.z, sq); sq = fmaf(v.w, v.w, sq);
+          xs[j] = v;
+        }
+      }
+    }
+  }
+  if (d.rms) {
+    // reference rmsnorm (src/seq.cpp:3-16): ss = 1/sqrtf(sum/size + 1e-5f); the block sum
+    // is taken in a fixed order (waves 0..PW-1), so every block gets the same ss
+    sq = wave_sum(sq);
+    if (lane == 0) red[wave] = sq;
+    __syncthreads();
+    float t = red[0];
+#pragma unroll
+    for (int w = 1; w < PW; ++w) t += red[w];
+    const float s = __fdiv_rn(1.0f, sqrtf(__fadd_rn(__fdiv_rn(t, (float)d.K), 1e-5f)));
+    const f4* w4 = reinterpret_cast<const f4*>(rmsw);
+    for (int j = threadIdx.x; j < n4; j += PT) {
+      const f4 w = w4[j];
+      const f4 v = xs[j];
+      xs[j] = f4{__fmul_rn(w.x, __fmul_rn(s, v.x)), __fmul_rn(w.y, __fmul_rn(s, v.y)),
+                 __fmul_rn(w.z, __fmul_rn(s, v.z)), __fmul_rn(w.w, __fmul_rn(s, v.w))};
+    }
+  }
+  __syncthreads();
+}
+
+// Control wave, while the others stream: the next norm's weights into LDS (constants; only
+// the staging reads rmsw, and it has finished).
+TL_DEVICE void preload_rms(const float* w, int dim, float* rmsw, int lane) {
+  const f4* s4 = reinterpret_cast<const f4*>(w);
+  f4* d4 = reinterpret_cast<f4*>(rmsw);
+  for (int j = lane; j < (dim >> 2); j += 64) d4[j] = s4[j];
+}
+
+// Control wave: row values from the LDS row-chunk sums, fused epilogue, granule stores.
+// xres: this block's slice of the residual stream x (rows i0.. of the dim-row phases, the
+// same slice for Wo and W2), kept in LDS so the residual add never re-reads x.
+TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const float* res, float* xres, int lane,
+                        int l) {
+  unsigned long long best = 0;
+  for (int it = lane; it < g.ni; it += 64) {
+    float v[2] = {0.f, 0.f};
+    for (int r = 0; r < d.rpi; ++r) {
+      const float* rr = res + (it * d.rpi + r) * g.nch;
+      float s = rr[0];
+      for (int c = 1; c < g.nch; ++c) s = __fadd_rn(s, rr[c]);
+      v[r] = s;
+    }
+    const int item = g.i0 + it;
+    if (d.kind == PK_CLS) {
+      p.logits[item] = v[0];  // read by the host after the launch only
+      const unsigned long long k = argmax_pack(v[0], item);
+      best = k > best ? k : best;
+    } else if (d.kind == PK_WO || d.kind == PK_DOWN) {
+      xres[it] = __fadd_rn(xres[it], v[0]);  // residual (src/seq.cpp:139-141, 163-166)
+      st8_sc1(d.gout + item, gran(d.tag_out, xres[it]));
+      if (d.kind == PK_DOWN && l == p.L - 1) p.x[item] = xres[it];  // final residual stream (state)
+    } else if (d.kind == PK_UP) {
+      st8_sc1(d.gout + item, gran(d.tag_out, silu_mul(v[0], v[1])));
+    } else {  // PK_QKV: RoPE (src/seq.cpp:86-101), q / k_new / v_new granules, KV-cache row
+      const int row = 2 * item;
+      const int pb = p.pos[0];
+      float a0 = v[0], a1 = v[1];
+      if (row < p.dim + p.kvd) {
+        const int i = row < p.dim ? row : row - p.dim;
+        const float2 cs = p.rope[(long long)pb * (p.hs >> 1) + ((i % p.hs) >> 1)];
+        const float r0 = __fsub_rn(__fmul_rn(a0, cs.x), __fmul_rn(a1, cs.y));
+        const float r1 = __fadd_rn(__fmul_rn(a0, cs.y), __fmul_rn(a1, cs.x));
+        a0 = r0; a1 = r1;
+      }
+      st_gran2(rsrc_of(d.gout), (unsigned)row * 8u, d.tag_out, a0, a1);
+      if (row >= p.dim) {  // the cache row for later steps (this launch reads the granules)
+        int rk = row - p.dim;
+        float* base = p.kc;
+        if (rk >= p.kvd) { rk -= p.kvd; base = p.vc; }
+        *reinterpret_cast<float2*>(base + ((long long)l * p.S + pb) * p.kvd + rk) = make_float2(a0, a1);
+      }
+    }
+  }
+  if (d.kind == PK_CLS) {
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long other = __shfl_xor(best, o, 64);
+      best = other > best ? other : best;
+    }
+    if (lane == 0) st8_sc1(p.bmax + blockIdx.x, best);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drained before the final arrival
+  }
+}
+
+// Sharded-counter grid barrier (the final one only).  Callers have drained every storing
+// wave.  One lane per block adds to its shard; lanes 0..7 of wave 0 poll the eight shards.
+TL_DEVICE void grid_barrier(const PStep& p) {
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const int G = gridDim.x;
+    if (lane == 0)
+      __hip_atomic_fetch_add(as_g32(p.sync + (blockIdx.x & 7) * 32), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int sh = lane & 7;
+    const unsigned need = (unsigned)((G - sh + 7) >> 3);
+    const unsigned* word = lane < 8 ? p.sync + sh * 32 : p.err;
+    for (unsigned spins = 0;; ++spins) {
+      const unsigned v = __hip_atomic_load(as_g32(word), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__all(lane >= 8 || v >= need)) break;
+      if (__any(lane == 8 && v != 0)) break;  // a wait already gave up: do not wait again
+      if (spins > kSpinLimit) {
+        if (lane == 0) __hip_atomic_store(as_g32(p.err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+}
+
+// Optional timeline (PStep::trace): the control wave of every block stamps the 100-MHz
+// real-time clock at phase start, input staged, all slots reduced, epilogue issued.
+#define TRACE(k)                                                                                \
+  do {                                                                                          \
+    if (p.trace && lane == 0)                                                                   \
+      p.trace[((long long)blockIdx.x * nph + ph) * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
+// The phase sequence as seen by one wave.  ROLE0 = the control wave (epilogues, attention,
+// norm preloads); the other waves stream.  Both execute the same workgroup barriers.
+template <int HS, bool ROLE0>
+TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* res, float* xres, float* red,
+                      float* rmsw, f4* xs, unsigned tb) {
+  const int G = gridDim.x;
+  const int nph = 5 * p.L + 1;
+  if constexpr (ROLE0) {
+    // this block's slice of the residual stream starts as the token's embedding row
+    const PGeo gx = geo(make_desc(p, PK_WO, 0, tb));
+    const float* er = p.emb + (long long)p.tok[0] * p.dim + gx.i0;
+    for (int it = lane; it < gx.ni; it += 64) xres[it] = er[it];
+    preload_rms(p.L > 0 ? p.rms_att : p.rms_final, p.dim, rmsw, lane);
+    __syncthreads();  // first norm weights preloaded
+    for (int ph = 0; ph < nph; ++ph) {
+      const int l = ph / 5;
+      const int kind = ph == nph - 1 ? PK_CLS : ph % 5;
+      TRACE(0);
+      if (kind == PK_ATTN) {
+        // one wave per (head, key-split) unit: unit u on block u % G
+        AttnWaveParams aw;
+        aw.a.q = p.xb; aw.a.kc = p.kc; aw.a.vc = p.vc;  // (q comes from the granules)
+        aw.a.kv_b_stride = (long long)p.L * p.S * p.kvd;
+        aw.a.kv_l_off = (long long)l * p.S * p.kvd;
+        aw.a.pos = p.pos; aw.a.out = p.xb; aw.a.part = p.part;
+        aw.a.dim = p.dim; aw.a.kv_dim = p.kvd; aw.a.head_size = HS; aw.a.n_heads = p.H;
+        aw.a.kv_mul = p.kv_mul; aw.a.seq_len = p.S; aw.a.nsplit = p.NS; aw.a.min_chunk = 16;
+        aw.cnt = p.tickets + (long long)l * p.H; aw.B = 1; aw.NS = p.NS;
+        aw.gqkv = p.gqkv; aw.gout = p.gxb;
+        aw.tag_in = tb + 5u * l + 1; aw.tag_out = tb + 5u * l + 2; aw.err = p.err;
+        const int units = p.H * p.NS;
+        for (int u = blockIdx.x; u < units; u += G) attn_unit<HS, 16, true>(aw, u, strips, lane);
+        TRACE(3);
+        continue;
+      }
+      const PDesc d = make_desc(p, kind, l, tb);
+      const PGeo g = geo(d);
+      stage(d, g, p, xs, rmsw, red, wave, lane);
+      TRACE(1);
+      if (kind == PK_QKV) preload_rms(p.rms_ffn + (long long)l * p.dim, p.dim, rmsw, lane);
+      if (kind == PK_UP) preload_rms(l + 1 < p.L ? p.rms_att + (long long)(l + 1) * p.dim : p.rms_final, p.dim, rmsw, lane);
+      __syncthreads();  // every slot reduced into res
+      TRACE(2);
+      epilogue(d, g, p, res, xres, lane, l);
+      TRACE(3);
+    }
+  } else {
+    const int sw = wave - 1;
+    f4 A[PL], B[PL];
+    __syncthreads();  // first norm weights preloaded
+    {
+      const PDesc d0 = make_desc(p, p.L > 0 ? PK_QKV : PK_CLS, p.L > 0 ? 0 : p.L, tb);
+      const PGeo g0 = geo(d0);
+      load_slot(d0, g0, p, sw, lane, A);
+      load_slot(d0, g0, p, sw + NSW, lane, B);
+    }
+    for (int ph = 0; ph < nph; ++ph) {
+      const int l = ph / 5;
+      const int kind = ph == nph - 1 ? PK_CLS : ph % 5;
+      if (kind == PK_ATTN) continue;
+      const PDesc d = make_desc(p, kind, kind == PK_CLS ? p.L : l, tb);
+      const PGeo g = geo(d);
+      stage(d, g, p, xs, rmsw, red, wave, lane);
+      run_gemv(d, g, p, sw, lane, xs, res, A, B);
+      if (kind != PK_CLS) {
+        const PDesc nd = next_desc(p, kind, l, tb);
+        const PGeo ng = geo(nd);
+        load_slot(nd, ng, p, sw, lane, A);
+        load_slot(nd, ng, p, sw + NSW, lane, B);
+      }
+      __syncthreads();  // every slot reduced into res
+    }
+  }
+  grid_barrier(p);
+  if constexpr (ROLE0) {
+    if (blockIdx.x != 0) return;
+    unsigned long long best = 0;
+    if (p.argmax) {
+      // argmax over the per-block winners + advance (src/llama.cpp:275-286)
+      for (int i = lane; i < G; i += 64) {
+        const unsigned long long k = ld8_sc1(p.bmax + i);
+        best = k > best ? k : best;
+      }
+      for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long other = __shfl_xor(best, o, 64);
+        best = other > best ? other : best;
+      }
+    }
+    if (lane == 0) {
+      p.seq[0] = (tb >> 12) + 1;  // every block read the sequence before the final barrier
+      if (p.argmax) {
+        const int next = best ? (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull)) : 0;
+        const int pp = p.pos[0];
+        if (p.out && pp < p.S) p.out[pp] = next;
+        p.tok[0] = next;
+        p.pos[0] = pp + 1;
+      }
+    }
+  }
+}
+
+template <int HS>
+__global__ void __launch_bounds__(PT) persistent_step_kernel(PStep p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* strips = reinterpret_cast<float*>(smem);  // 64: attention score strip of wave 0
+  float* xres = strips + 64;                        // kPResidFloats: residual slice
+  float* res = xres + kPResidFloats;                // kPResFloats: row-chunk sums
+  float* red = res + kPResFloats;                   // 16: block reductions
+  float* rmsw = red + 16;                           // dim: the next norm's weights
+  f4* xs = reinterpret_cast<f4*>(rmsw + p.dim);     // pad_floats: the staged input
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const unsigned tb = p.seq[0] << 12;  // tag base of this launch
+  if (wave == 0) phases<HS, true>(p, wave, lane, strips, res, xres, red, rmsw, xs, tb);
+  else phases<HS, false>(p, wave, lane, strips, res, xres, red, rmsw, xs, tb);
+}
+
+static size_t lds_bytes(const PStep& p) {
+  return (size_t)(64 + kPResidFloats + kPResFloats + 16 + p.dim + p.pad_floats) * 4;
+}
+
+bool persistent_prepare(PStep& p, int ncu, const char** why) {
+  auto fail = [&](const char* m) { if (why) *why = m; return false; };
+  if (p.hs != 64 && p.hs != 128) return fail("head size must be 64 or 128");
+  if (p.dim % 256 || p.hid % 256) return fail("dim and hidden_dim must be multiples of 256");
+  if (p.NS < 1 || p.NS > kMaxNS) return fail("attention splits out of range");
+  if (ncu < 8) return fail("too few compute units");
+  if (5 * p.L + 1 >= 4096) return fail("too many layers for the phase tags");
+  auto nchunks = [](int K) { return (K + PL * 256 - 1) / (PL * 256); };
+  auto padf = [&](int K) { return nchunks(K) * PL * 256; };
+  auto nrc = [&](int K, int n_items, int rpi) { return ((n_items + ncu - 1) / ncu) * rpi * nchunks(K); };
+  p.pad_floats = padf(p.dim) > padf(p.hid) ? padf(p.dim) : padf(p.hid);
+  if (nrc(p.dim, (p.dim + 2 * p.kvd) / 2, 2) > kPResFloats || nrc(p.dim, p.hid, 2) > kPResFloats ||
+      nrc(p.hid, p.dim, 1) > kPResFloats || nrc(p.dim, p.V, 1) > kPResFloats)
+    return fail("too many rows per block");
+  if ((p.dim + ncu - 1) / ncu > kPResidFloats) return fail("residual slice per block too large");
+  if (lds_bytes(p) > 160 * 1024) return fail("activations do not fit the LDS");
+  static bool attr_set = false;
+  if (!attr_set) {  // allow more than 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
+    if (hipFuncSetAttribute((const void*)persistent_step_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess ||
+        hipFuncSetAttribute((const void*)persistent_step_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess)
+      return fail("cannot raise the dynamic LDS limit");
+    attr_set = true;
+  }
+  int nb = 0;
+  const hipError_t e = p.hs == 128
+      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, persistent_step_kernel<128>, PT, lds_bytes(p))
+      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, persistent_step_kernel<64>, PT, lds_bytes(p));
+  if (e != hipSuccess || nb < 1) return fail("persistent kernel does not fit one block per CU");
+  return true;
+}
+
+// The caller zeroes p.sync (kPSyncWords) and the tickets on the same stream right before.
+hipError_t launch_persistent_step(const PStep& p, hipStream_t s, int ncu) {
+  if (p.hs == 128)
+    hipLaunchKernelGGL(persistent_step_kernel<128>, dim3(ncu), dim3(PT), lds_bytes(p), s, p);
+  else
+    hipLaunchKernelGGL(persistent_step_kernel<64>, dim3(ncu), dim3(PT), lds_bytes(p), s, p);
+  return hipGetLastError();
+}
+
+}  // namespace tl

@@ -1,0 +1,38 @@
+// persist.hpp — the one-launch decode step (persist.hip) for batch 1, fp32 weights.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace tl {
+
+struct PStep {
+  // weights (reference TransformerWeights, include/models.hpp)
+  const float *emb, *rms_att, *rms_ffn, *wq, *wk, *wv, *wo, *w1, *w2, *w3, *rms_final, *wcls;
+  int dim, hid, kvd, L, S, V, H, kv_mul, hs, NS;
+  // run state
+  float *x, *xb, *logits, *kc, *vc, *part;
+  unsigned* tickets;        // attention combine tickets [L][H], zeroed before every launch
+  const float2* rope;       // [S][hs/2] (cos, sin)
+  int* tok;                 // [1] read at layer 0; rewritten by the argmax tail
+  int* pos;                 // [1] read everywhere; advanced by the argmax tail
+  int* out;                 // [S] greedy tokens by position (argmax tail), may be null
+  // hand-off granules {value, tag} (zero once at allocation; tags are never 0)
+  unsigned long long *gx, *gxb, *ghb, *gqkv;  // [dim], [dim], [hidden], [dim + 2*kv_dim]
+  unsigned* sync;           // kPSyncWords barrier shards, zeroed before every launch
+  unsigned* err;            // sticky: a wait gave up (1: barrier, 2: hand-off)
+  unsigned* seq;            // launch sequence (tags), advanced by the kernel
+  unsigned long long* bmax; // [grid] per-block classifier argmax
+  int argmax;               // run the argmax + advance tail
+  int pad_floats;           // LDS activation strip (floats), >= every phase's padded K
+  unsigned long long* trace; // optional [grid][5L+1][4] timeline (100-MHz clock), or null
+};
+
+constexpr int kPSyncWords = 8 * 32;   // 8 shard counters, one 128-B line each
+constexpr int kPResFloats = 1024;     // per-block row-chunk results (LDS)
+
+// Host: can this step run as one launch on `ncu` co-resident blocks?  Sets pad_floats.
+bool persistent_prepare(PStep& p, int ncu, const char** why);
+// Launch only: the caller zeroes p.sync (kPSyncWords) on stream s right before (a memset
+// node ahead of the kernel node when captured).
+hipError_t launch_persistent_step(const PStep& p, hipStream_t s, int ncu);
+
+}  // namespace tl

@@ -82,9 +82,9 @@ STATUS = {0: "SUCCESS", 1: "NOT_INITIALIZED", 2: "ALLOC_FAILED", 3: "INVALID_VAL
           9: "HANDLE_IS_NULLPTR", 10: "INVALID_ENUM", 11: "UNKNOWN"}
 
 # kernel classes (include/thallama.h)
-K_QKV, K_ATTN, K_WO, K_FFN_UP, K_FFN_DOWN, K_CLS, K_ARGMAX = range(7)
-K_NAMES = ["qkv", "attn", "wo", "ffn_up", "ffn_down", "cls", "argmax"]
-OPT_NT_WEIGHTS, OPT_ATTN_SPLITS, OPT_USE_GRAPH, OPT_PROFILE = 1, 2, 3, 4
+K_QKV, K_ATTN, K_WO, K_FFN_UP, K_FFN_DOWN, K_CLS, K_ARGMAX, K_STEP = range(8)
+K_NAMES = ["qkv", "attn", "wo", "ffn_up", "ffn_down", "cls", "argmax", "step"]
+OPT_NT_WEIGHTS, OPT_ATTN_SPLITS, OPT_USE_GRAPH, OPT_PROFILE, OPT_PERSISTENT = 1, 2, 3, 4, 5
 
 _lib = None
 
@@ -142,6 +142,8 @@ def lib():
                                             C.POINTER(RunState), c_int_p, c_int_p, P]),
             "thallama_decoder_destroy": (None, [VP]),
             "thallama_decoder_set": (I, [VP, I, I]),
+            "thallama_decoder_persistent": (I, [VP]),
+            "thallama_decoder_ptrace": (I, [VP, I, C.POINTER(C.c_ulonglong), C.c_size_t]),
             "thallama_decoder_stream": (VP, [VP]),
             "thallama_decoder_forward": (I, [VP, c_int_p, c_int_p, P]),
             "thallama_decoder_greedy": (I, [VP, c_int_p, c_int_p, I, c_int_p, I]),
@@ -374,6 +376,19 @@ class Decoder:
 
     def set(self, key, value):
         check(lib().thallama_decoder_set(self.h, key, int(value)), "decoder_set")
+
+    def persistent(self):
+        """True if steps run as one persistent launch (persist.hip)."""
+        return bool(lib().thallama_decoder_persistent(self.h))
+
+    def ptrace(self, enable=True):
+        """Enable the persistent-step timeline; returns the stamps of the last launch as a
+        [grid, phases, 4] uint64 array (100-MHz clock) once a launch has run."""
+        n = lib().thallama_decoder_ptrace(self.h, int(enable), None, 0)
+        check(0 if n >= 0 else n, "decoder_ptrace")
+        out = np.zeros(n, np.uint64)
+        lib().thallama_decoder_ptrace(self.h, 0, out.ctypes.data_as(C.POINTER(C.c_ulonglong)), n)
+        return out
 
     def forward(self, tokens, pos, want_logits=True):
         tok = (C.c_int * self.batch)(*[int(t) for t in tokens])

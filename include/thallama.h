@@ -32,12 +32,26 @@ enum {
   THALLAMA_OPT_ATTN_SPLITS = 2,  /* key splits per (head, seq); 0 = auto */
   THALLAMA_OPT_USE_GRAPH = 3,    /* 0/1: replay greedy steps from a captured hipGraph */
   THALLAMA_OPT_PROFILE = 4,      /* 0/1: HIP events around every kernel class (eager only) */
+  THALLAMA_OPT_PERSISTENT = 5,   /* 0/1: whole step as ONE persistent launch (batch 1, fp32,
+                                    head size 64/128; default 1 where supported).  Profiled
+                                    as the single class THALLAMA_K_STEP. */
 };
+
+/* 1 if the decoder runs its steps as one persistent launch (THALLAMA_OPT_PERSISTENT
+ * requested and the shape supported), else 0. */
+int thallama_decoder_persistent(thallama_decoder* d);
+/* Diagnostics: enable != 0 allocates a timeline buffer that every later persistent launch
+ * fills with 100-MHz clock stamps, [grid][5*n_layers+1][4] (phase start, input staged,
+ * slots reduced, epilogue drained); host != NULL copies up to n stamps out (synchronous).
+ * Returns the number of stamps per launch, or a negative error. */
+int thallama_decoder_ptrace(thallama_decoder* d, int enable, unsigned long long* host, size_t n);
 
 /* Kernel classes for profiling */
 enum {
   THALLAMA_K_QKV = 0, THALLAMA_K_ATTN = 1, THALLAMA_K_WO = 2, THALLAMA_K_FFN_UP = 3,
-  THALLAMA_K_FFN_DOWN = 4, THALLAMA_K_CLS = 5, THALLAMA_K_ARGMAX = 6, THALLAMA_K_COUNT = 7
+  THALLAMA_K_FFN_DOWN = 4, THALLAMA_K_CLS = 5, THALLAMA_K_ARGMAX = 6,
+  THALLAMA_K_STEP = 7,  /* the whole step as one persistent launch (THALLAMA_OPT_PERSISTENT) */
+  THALLAMA_K_COUNT = 8
 };
 
 /* w and s hold DEVICE pointers (as produced by copy_weight_to_device /

@@ -1,0 +1,82 @@
+"""Timeline of the persistent decode step (hip_llama.cpp_amd/csrc/persist.hip).
+
+Wave 0 of every block stamps the 100-MHz real-time clock at: phase start (grid barrier exit),
+input staged, all slots reduced, epilogue drained.  This prints, per phase kind averaged over
+layers (us): staging, streaming (staged -> reduced, the slowest block), epilogue, the barrier
+(last arrival -> first exit) and the whole phase, plus the per-phase weight bytes and the
+rate they imply.
+
+    python tools/persist_trace.py --model 7b --steps 4
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+from __graft_entry__ import _pkg  # noqa: E402
+
+MODELS = {"7b": (4096, 11008, 32, 32, 32, 32000, 2048), "110m": (768, 2048, 12, 12, 12, 32000, 1024)}
+KINDS = ["qkv", "attn", "wo", "ffn_up", "ffn_down"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="7b", choices=sorted(MODELS))
+    ap.add_argument("--pos", type=int, default=8, help="position of the traced step")
+    ap.add_argument("--json", default="")
+    args = ap.parse_args()
+    _pkg()
+    from hip_llama_cpp_amd import thallama as tl
+    cfg = MODELS[args.model]
+    c = tl.Config.make(*cfg)
+    model = tl.DeviceModel(c, 0, seed=7)
+    state = tl.DeviceState(c, 1)
+    dec = tl.Decoder(model, state)
+    assert dec.persistent()
+    dec.greedy([1], [0], args.pos, want_tokens=False)
+    dec.ptrace(True)
+    dec.greedy([1], [args.pos], 1, want_tokens=False)
+    t = dec.ptrace(False).astype(np.int64)
+    L = cfg[2]
+    nph = 5 * L + 1
+    G = t.size // (nph * 4)
+    t = t.reshape(G, nph, 4)
+    t = (t - t[:, 0, 0].min()) * 0.01  # us
+    dim, hid, kvd, V = cfg[0], cfg[1], cfg[0] * cfg[4] // cfg[3], cfg[5]
+    wbytes = {"qkv": 4 * dim * (dim + 2 * kvd), "attn": 0, "wo": 4 * dim * dim, "ffn_up": 8 * dim * hid,
+              "ffn_down": 4 * dim * hid, "cls": 4 * dim * V}
+    rows = {}
+    for ph in range(nph):
+        kind = "cls" if ph == nph - 1 else KINDS[ph % 5]
+        s0 = t[:, ph, 0]
+        end = t[:, ph, 3]
+        nxt = t[:, ph + 1, 0] if ph + 1 < nph else None
+        r = {"start_skew": s0.max() - s0.min(), "epi_max": (end - t[:, ph, 2]).max() if kind != "attn" else 0.0}
+        if kind != "attn":
+            r["stage"] = np.median(t[:, ph, 1] - s0)
+            r["stream_max"] = (t[:, ph, 2] - t[:, ph, 1]).max()
+        if nxt is not None:
+            r["barrier"] = nxt.min() - end.max()
+            r["phase"] = nxt.max() - s0.max()
+        rows.setdefault(kind, []).append(r)
+    out = {}
+    print(f"{args.model}: {G} blocks, step {t[:, -1, 3].max() - t[:, 0, 0].min():.1f} us")
+    print(f"{'kind':9s}{'phase':>8s}{'stage':>8s}{'stream':>8s}{'epi':>7s}{'barrier':>8s}{'skew':>7s}{'GB/s':>8s}")
+    for kind, rs in rows.items():
+        avg = {k: float(np.mean([r[k] for r in rs if k in r])) for k in rs[0]}
+        ph_us = avg.get("phase", float("nan"))
+        gbs = wbytes[kind] / (ph_us * 1e-6) / 1e9 if kind != "attn" and ph_us == ph_us else 0.0
+        print(f"{kind:9s}{ph_us:8.2f}{avg.get('stage', 0):8.2f}{avg.get('stream_max', 0):8.2f}"
+              f"{avg['epi_max']:7.2f}{avg.get('barrier', 0):8.2f}{avg['start_skew']:7.2f}{gbs:8.0f}")
+        out[kind] = avg
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
