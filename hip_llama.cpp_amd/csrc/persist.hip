@@ -484,6 +484,9 @@ bool persistent_prepare(PStep& p, int ncu, const char** why) {
   if (p.NS < 1 || p.NS > kMaxNS) return fail("attention splits out of range");
   if (ncu < 8) return fail("too few compute units");
   if (5 * p.L + 1 >= 4096) return fail("too many layers for the phase tags");
+  // every block must own work in every phase: a hand-off buffer may be rewritten as soon as
+  // the next phase's outputs are complete, which then implies every block has staged it
+  if (p.dim < ncu || (p.dim + 2 * p.kvd) / 2 < ncu || p.hid < ncu) return fail("model too small for the grid");
   auto nchunks = [](int K) { return (K + PL * 256 - 1) / (PL * 256); };
   auto padf = [&](int K) { return nchunks(K) * PL * 256; };
   auto nrc = [&](int K, int n_items, int rpi) { return ((n_items + ncu - 1) / ncu) * rpi * nchunks(K); };

@@ -73,6 +73,14 @@ def main():
         print(f"{kind:9s}{ph_us:8.2f}{avg.get('stage', 0):8.2f}{avg.get('stream_max', 0):8.2f}"
               f"{avg['epi_max']:7.2f}{avg.get('barrier', 0):8.2f}{avg['start_skew']:7.2f}{gbs:8.0f}")
         out[kind] = avg
+    # where the skew comes from: per-block streaming time of the big phases, by blockIdx % 8
+    # (blocks b and b+8 share an XCD under round-robin dispatch) and over the grid
+    for kind, k in (("ffn_up", 3), ("qkv", 0), ("ffn_down", 4)):
+        st = np.mean([t[:, ph, 2] - t[:, ph, 1] for ph in range(k, nph - 1, 5)], axis=0)
+        byx = [float(np.mean(st[x::8])) for x in range(8)]
+        print(f"{kind:9s} stream per block: min {st.min():.2f} med {np.median(st):.2f} max {st.max():.2f}; "
+              f"by blockIdx%8: " + " ".join(f"{v:.1f}" for v in byx))
+        out[kind + "_stream_by_xcd"] = byx
     if args.json:
         with open(args.json, "w") as f:
             json.dump(out, f, indent=1)
