@@ -1,0 +1,288 @@
+// run.cpp — the reference's `run` CLI (src/llama.cpp:1486-1639) on the MI355X library.
+//
+//   run <model.bin> [-t temp] [-p topp] [-s seed] [-n steps] [-i prompt] [-z tokenizer]
+//                   [-m generate|chat|test] [-y system] [-f input] [-o output] [-b batch]
+//
+// Same flags, defaults, validation and output files.  What differs is underneath:
+//  * the model is read once (mmap, src/utils.cpp:150-170 semantics), uploaded to GPU 0 with
+//    ONE copy and replicated to every other GPU with an RCCL broadcast over xGMI (the
+//    reference uploads the full model from host memory once per GPU thread);
+//  * every decode step is the fused decoder of libthallama.so (the persistent one-launch step
+//    at batch 1), not 1300+ small launches;
+//  * `generate` runs on the GPU (the reference's generate() uses the CPU forward);
+//  * the host side — tokenizer, sampler, request files and the test-mode scheduler — is
+//    libthallama_host.so (include/thallama_host.h), byte-for-byte the reference's.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/models.hpp"
+#include "../../include/thallama.h"
+#include "../../include/thallama_host.h"
+
+#define HIP_OK(cmd)                                                                              \
+  do {                                                                                           \
+    hipError_t e_ = (cmd);                                                                       \
+    if (e_ != hipSuccess) {                                                                      \
+      fprintf(stderr, "HIP error %s at %s:%d: %s\n", hipGetErrorString(e_), __FILE__, __LINE__, #cmd); \
+      exit(EXIT_FAILURE);                                                                        \
+    }                                                                                            \
+  } while (0)
+#define NCCL_OK(cmd)                                                                             \
+  do {                                                                                           \
+    ncclResult_t r_ = (cmd);                                                                     \
+    if (r_ != ncclSuccess) {                                                                     \
+      fprintf(stderr, "RCCL error %s at %s:%d\n", ncclGetErrorString(r_), __FILE__, __LINE__);  \
+      exit(EXIT_FAILURE);                                                                        \
+    }                                                                                            \
+  } while (0)
+
+static long time_in_ms() {
+  struct timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  return ts.tv_sec * 1000 + ts.tv_nsec / 1000000;
+}
+
+static void error_usage() {
+  fprintf(stderr, "Usage:   run <checkpoint> [options]\n");
+  fprintf(stderr, "Example: run model.bin -n 256 -i \"Once upon a time\"\n");
+  fprintf(stderr, "Example: run model.bin -m test -f <input_filename> -o <output_filename>\n");
+  fprintf(stderr, "Options:\n");
+  fprintf(stderr, "  -t <float>  temperature in [0,inf], default 1.0 (ignore the arg for test mode)\n");
+  fprintf(stderr, "  -p <float>  p value in top-p (nucleus) sampling in [0,1] default 0.9 (ignore the arg for test mode)\n");
+  fprintf(stderr, "  -s <int>    random seed, default time(NULL) (ignore the arg for test mode)\n");
+  fprintf(stderr, "  -n <int>    number of steps to run for, default 256. 0 = max_seq_len (for test mode steps = max_seq_len)\n");
+  fprintf(stderr, "  -i <string> input prompt (ignore the arg for test mode)\n");
+  fprintf(stderr, "  -z <string> optional path to custom tokenizer\n");
+  fprintf(stderr, "  -m <string> mode: generate|chat|test, default: generate\n");
+  fprintf(stderr, "  -y <string> (optional) system prompt in chat mode\n");
+  fprintf(stderr, "  -f <string> (only for test mode) input filename\n");
+  fprintf(stderr, "  -o <string> (only for test mode) output filename\n");
+  fprintf(stderr, "  -b <string> batch size\n");
+  exit(EXIT_FAILURE);
+}
+
+// One GPU's replica: weights (an arena view), run state for `batch` sequences, the decoder.
+struct Replica {
+  int dev = 0;
+  TransformerWeights w{};
+  RunState* s = nullptr;
+  thallama_decoder* dec = nullptr;
+};
+
+// Weights on every device: one H2D copy to device 0, then an RCCL broadcast (in 1 GiB
+// pieces) into every other device's arena.  Returns the per-device weight views.
+static std::vector<Replica> replicate(Transformer* t, int n_dev, int batch) {
+  const int shared = t->weights.wcls == t->weights.token_embedding_table;
+  const size_t n = thallama_v0_payload_floats(&t->config, shared);
+  std::vector<Replica> reps((size_t)n_dev);
+  std::vector<float*> arena((size_t)n_dev, nullptr);
+  for (int d = 0; d < n_dev; ++d) {
+    HIP_OK(hipSetDevice(d));
+    HIP_OK(hipMalloc(&arena[d], n * sizeof(float)));
+  }
+  HIP_OK(hipSetDevice(0));
+  HIP_OK(hipMemcpy(arena[0], t->weights.token_embedding_table, n * sizeof(float), hipMemcpyHostToDevice));
+  if (n_dev > 1) {
+    std::vector<ncclComm_t> comms((size_t)n_dev);
+    std::vector<int> devs((size_t)n_dev);
+    for (int d = 0; d < n_dev; ++d) devs[d] = d;
+    NCCL_OK(ncclCommInitAll(comms.data(), n_dev, devs.data()));
+    std::vector<hipStream_t> st((size_t)n_dev);
+    for (int d = 0; d < n_dev; ++d) {
+      HIP_OK(hipSetDevice(d));
+      HIP_OK(hipStreamCreate(&st[d]));
+    }
+    const size_t piece = (size_t)1 << 28;  // floats (1 GiB)
+    for (size_t off = 0; off < n; off += piece) {
+      const size_t cnt = n - off < piece ? n - off : piece;
+      NCCL_OK(ncclGroupStart());
+      for (int d = 0; d < n_dev; ++d)
+        NCCL_OK(ncclBroadcast(arena[0] + off, arena[d] + off, cnt, ncclFloat, 0, comms[d], st[d]));
+      NCCL_OK(ncclGroupEnd());
+    }
+    for (int d = 0; d < n_dev; ++d) {
+      HIP_OK(hipSetDevice(d));
+      HIP_OK(hipStreamSynchronize(st[d]));
+      HIP_OK(hipStreamDestroy(st[d]));
+      ncclCommDestroy(comms[d]);
+    }
+  }
+  for (int d = 0; d < n_dev; ++d) {
+    HIP_OK(hipSetDevice(d));
+    Replica& r = reps[d];
+    r.dev = d;
+    thallama_map_weights(&r.w, &t->config, arena[d], shared);
+    alloc_state_to_device_batch(t, &r.s, batch);
+    if (thallama_decoder_create(&r.dec, &t->config, &r.w, r.s, batch, nullptr) != 0) {
+      fprintf(stderr, "decoder on device %d: %s\n", d, thallama_last_error());
+      exit(EXIT_FAILURE);
+    }
+  }
+  return reps;
+}
+
+static void release(std::vector<Replica>& reps) {
+  for (auto& r : reps) {
+    HIP_OK(hipSetDevice(r.dev));
+    thallama_decoder_destroy(r.dec);
+    free_state_device(r.s);
+    HIP_OK(hipFree(r.w.token_embedding_table));
+  }
+}
+
+// test mode step callback: worker w drives replica w
+static int replica_step(void* ctx, int worker, int batch, const int* token, const int* pos, float* logits) {
+  Replica& r = (*(std::vector<Replica>*)ctx)[worker];
+  if (hipSetDevice(r.dev) != hipSuccess) return -3;
+  (void)batch;
+  const int st = thallama_decoder_forward(r.dec, token, pos, logits);
+  if (st) fprintf(stderr, "device %d step: %s\n", r.dev, thallama_last_error());
+  return st;
+}
+
+// generate mode (src/llama.cpp:522-579), on GPU 0
+static void generate(Transformer* t, Replica& r, thallama_tokenizer* tok, thallama_sampler* smp, const char* prompt,
+                     int steps) {
+  if (!prompt) prompt = "";
+  std::vector<int> ids(strlen(prompt) + 3);
+  int n_ids = 0;
+  thallama_tokenizer_encode(tok, prompt, 1, 0, ids.data(), &n_ids);
+  if (n_ids < 1) {
+    fprintf(stderr, "something is wrong, expected at least 1 prompt token\n");
+    exit(EXIT_FAILURE);
+  }
+  std::vector<float> logits((size_t)t->config.vocab_size);
+  long start = 0;
+  int token = ids[0], pos = 0;
+  while (pos < steps) {
+    if (thallama_decoder_forward(r.dec, &token, &pos, logits.data()) != 0) {
+      fprintf(stderr, "forward: %s\n", thallama_last_error());
+      exit(EXIT_FAILURE);
+    }
+    const int next = pos < n_ids - 1 ? ids[pos + 1] : thallama_sample(smp, logits.data());
+    pos++;
+    if (next == 1) break;  // BOS delimits sequences
+    const char* piece = thallama_tokenizer_decode(tok, token, next);
+    if (thallama_piece_is_safe(piece)) printf("%s", piece);
+    fflush(stdout);
+    token = next;
+    if (start == 0) start = time_in_ms();
+  }
+  printf("\n");
+  if (pos > 1) {
+    const long end = time_in_ms();
+    fprintf(stderr, "achieved tok/s: %f\n", (pos - 1) / (double)(end - start) * 1000);
+  }
+}
+
+int main(int argc, char* argv[]) {
+  const long total_start = time_in_ms();
+  char* checkpoint_path = nullptr;
+  const char* tokenizer_path = "./assets/tokenizer.bin";
+  float temperature = 1.0f, topp = 0.9f;
+  int steps = 256, batch = 1;
+  const char* prompt = nullptr;
+  unsigned long long rng_seed = 0;
+  const char* mode = "generate";
+  const char* input_filename = nullptr;
+  const char* output_filename = nullptr;
+
+  if (argc >= 2) checkpoint_path = argv[1];
+  else error_usage();
+  for (int i = 2; i < argc; i += 2) {
+    if (i + 1 >= argc || argv[i][0] != '-' || strlen(argv[i]) != 2) error_usage();
+    const char* v = argv[i + 1];
+    switch (argv[i][1]) {
+      case 't': temperature = (float)atof(v); break;
+      case 'p': topp = (float)atof(v); break;
+      case 's': rng_seed = (unsigned long long)atoi(v); break;
+      case 'n': steps = atoi(v); break;
+      case 'i': prompt = v; break;
+      case 'z': tokenizer_path = v; break;
+      case 'm': mode = v; break;
+      case 'y': break;  // chat system prompt (chat mode is disabled in the reference)
+      case 'f': input_filename = v; break;
+      case 'o': output_filename = v; break;
+      case 'b': batch = atoi(v); break;
+      default: error_usage();
+    }
+  }
+  if (rng_seed <= 0) rng_seed = (unsigned int)time(nullptr);
+  if (temperature < 0.0) temperature = 0.0;
+  if (topp < 0.0 || 1.0 < topp) topp = 0.9;
+  if (steps < 0) steps = 0;
+  if (batch < 1) batch = 1;
+
+  Transformer transformer;
+  build_transformer(&transformer, checkpoint_path);
+  if (steps == 0 || steps > transformer.config.seq_len) steps = transformer.config.seq_len;
+  const int V = transformer.config.vocab_size;
+  thallama_tokenizer* tok = thallama_tokenizer_load(tokenizer_path, V);
+  if (!tok) {
+    fprintf(stderr, "couldn't load %s\n", tokenizer_path);
+    exit(EXIT_FAILURE);
+  }
+  thallama_sampler* smp = thallama_sampler_create(V, temperature, topp, rng_seed);
+
+  if (strcmp(mode, "generate") == 0) {
+    std::vector<Replica> reps = replicate(&transformer, 1, 1);
+    generate(&transformer, reps[0], tok, smp, prompt, steps);
+    release(reps);
+  } else if (strcmp(mode, "chat") == 0) {
+    // chat() is commented out in the reference's main (src/llama.cpp:1590)
+  } else if (strcmp(mode, "test") == 0) {
+    steps = transformer.config.seq_len;
+    if (!input_filename || !output_filename) error_usage();
+    const int max_token_len = thallama_tokenizer_max_token_length(tok);
+    printf("max_token_len: %d, max_seq_len: %d\n", max_token_len, steps);
+    thallama_requests* req = thallama_requests_read(input_filename, max_token_len, steps);
+    if (!req) {
+      fprintf(stderr, "cannot open the file: %s\n", input_filename);
+      exit(EXIT_FAILURE);
+    }
+    printf("requests size = %lu B\n",
+           (unsigned long)(((size_t)thallama_requests_count(req) * max_token_len * steps + 1) * 2));
+    int n_dev = 0;
+    HIP_OK(hipGetDeviceCount(&n_dev));
+    fprintf(stderr, "\n DATA PARALLELISM \n");
+    fprintf(stderr, "\n Num Devices %d\n", n_dev);
+    fprintf(stderr, "\n Batch Size %d\n", batch);
+    const long load_start = time_in_ms();
+    std::vector<Replica> reps = replicate(&transformer, n_dev, batch);
+    fprintf(stdout, "\nLoad model time (1 upload + RCCL broadcast to %d GPUs): %f\n", n_dev,
+            (double)(time_in_ms() - load_start) / 1000);
+
+    const long start = time_in_ms();
+    long long num_gen_tokens = 0;
+    const int st = thallama_serve_requests(req, tokenizer_path, V, n_dev, batch, replica_step, &reps, &num_gen_tokens);
+    const long end = time_in_ms();
+    if (st != 0) {
+      fprintf(stderr, "test mode failed (%d)\n", st);
+      exit(EXIT_FAILURE);
+    }
+    fprintf(stdout, "Total achieved token: %lld\n", num_gen_tokens);
+    fprintf(stdout, "elapsed time(s): %f, achieved throughput(tok/s): %f\n", (double)(end - start) / 1000,
+            num_gen_tokens / (double)(end - start) * 1000);
+    if (thallama_requests_write(req, output_filename) != 0) {
+      fprintf(stderr, "cannot write output file: %s\n", input_filename);
+      exit(EXIT_FAILURE);
+    }
+    thallama_requests_free(req);
+    release(reps);
+  } else {
+    fprintf(stderr, "unknown mode: %s\n", mode);
+    error_usage();
+  }
+  thallama_sampler_free(smp);
+  thallama_tokenizer_free(tok);
+  free_transformer(&transformer);
+  fprintf(stdout, "total elapsed time(s): %lf\n", (double)(time_in_ms() - total_start) / 1000);
+  return 0;
+}

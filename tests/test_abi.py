@@ -10,18 +10,23 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(REPO, "hip_llama.cpp_amd", "lib", "libthallama.so")
+HOST_LIB = os.path.join(REPO, "hip_llama.cpp_amd", "lib", "libthallama_host.so")
+HOST_HEADERS = ("thallama_host.h",)  # exported by the CPU-only libthallama_host.so
 
 
-def declared_functions():
+def declared_functions(host=False):
     names = set()
     pat = re.compile(r"^\s*(?:[A-Za-z_][\w\s\*]*?)\b([A-Za-z_]\w*)\s*\(", re.M)
     for h in glob.glob(os.path.join(REPO, "include", "**", "*.h*"), recursive=True):
         if h.endswith("thallama_synth.h") or h.endswith("hip_helper.hpp"):
             continue  # header-only helpers / macros
+        if h.endswith(HOST_HEADERS) != host:
+            continue
         src = open(h).read()
         src = re.sub(r"//.*", "", src)
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         src = re.sub(r"#.*", "", src)
+        src = re.sub(r"typedef[^;]*;", "", src)  # function-pointer typedefs are not entry points
         for m in pat.finditer(src):
             name = m.group(1)
             if name in ("if", "for", "while", "return", "sizeof", "defined", "__attribute__"):
@@ -30,8 +35,8 @@ def declared_functions():
     return sorted(names)
 
 
-def exported():
-    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+def exported(lib=LIB):
+    out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
     return {line.split()[-1] for line in out.splitlines() if " T " in line}
 
 
@@ -45,6 +50,17 @@ def test_every_declared_symbol_is_exported_unmangled():
     assert len(decl) > 40
     missing = [n for n in decl if n not in syms]
     assert not missing, f"declared but not exported with C linkage: {missing}"
+
+
+def test_host_library_exports_its_header():
+    assert os.path.exists(HOST_LIB), "run __graft_entry__.build() first"
+    syms, decl = exported(HOST_LIB), declared_functions(host=True)
+    assert len(decl) > 20
+    missing = [n for n in decl if n not in syms]
+    assert not missing, f"declared but not exported with C linkage: {missing}"
+    # CPU only: no HIP runtime dependency
+    out = subprocess.run(["ldd", HOST_LIB], capture_output=True, text=True).stdout
+    assert "amdhip" not in out
 
 
 def test_ctypes_binds_without_gpu(tl):

@@ -1,0 +1,216 @@
+"""The reference CLI's host side (include/thallama_host.h, hip_llama.cpp_amd/host/host.cpp) against
+the reference's own code:
+  * tokenizer known-answer tests of the reference's test.c;
+  * encode / decode / append_str filter / sample() against fixtures produced by the reference's
+    run.cc tokenizer + sampler (tests/golden/make_host_golden.py) and, where oracle/_ref exists,
+    against that live build on fuzzed inputs;
+  * request files and the test-mode scheduler (src/llama.cpp:424-505, 891-1083).
+All bit-exact (integers, bytes, and the sampler's float arithmetic).  CPU only.
+"""
+import ctypes as C
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(REPO, "tests", "golden")
+TOK = os.path.join(GOLD, "tokenizer.bin")
+REF_RUN = os.path.join(REPO, "oracle", "_ref", "librun.so")
+V = 32000
+
+
+@pytest.fixture(scope="module")
+def host(pkg):
+    from hip_llama_cpp_amd import host as H
+    H.lib()
+    return H
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with open(os.path.join(GOLD, "host_golden.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def tok(host):
+    return host.Tokenizer(TOK, V)
+
+
+@pytest.fixture(scope="module")
+def ref():
+    if not os.path.exists(REF_RUN):
+        pytest.skip("oracle/_ref/librun.so not built (reference tree absent)")
+    import sys
+    sys.path.insert(0, GOLD)
+    import make_host_golden as M
+    L = M.ref()
+    return L, L.ref_tok_load(TOK.encode(), V)
+
+
+def test_reference_copies_identical():
+    """run.cc's tokenizer/sampler (the compiled oracle) == src/llama.cpp's (the live reference)."""
+    a_p, b_p = "/root/reference/run.cc", "/root/reference/src/llama.cpp"
+    if not (os.path.exists(a_p) and os.path.exists(b_p)):
+        pytest.skip("reference tree absent")
+
+    def body(src, name):
+        m = re.search(r"\n[^\n]*\b" + name + r"\(([^)]*)\)\s*\{", src)
+        i, depth = m.end(), 1
+        while depth:
+            depth += (src[i] == "{") - (src[i] == "}")
+            i += 1
+        return re.sub(r"\s+", " ", re.sub(r"//[^\n]*", "", src[m.start():i]))
+    a, b = open(a_p).read(), open(b_p).read()
+    for name in ["build_tokenizer", "decode", "append_str", "str_lookup", "encode", "sample_argmax", "sample_mult",
+                 "compare", "sample_topp", "build_sampler", "random_u32", "random_f32", "sample"]:
+        assert body(a, name) == body(b, name), name
+
+
+def test_tokenizer_kat(tok, golden):
+    """The reference's test.c cases (Llama 2 example prompts + the empty string)."""
+    assert tok.max_token_length == 27
+    assert len(golden["kat"]) == 5
+    for k in golden["kat"]:
+        assert tok.encode(k["text"]) == k["ids"], k["text"]
+
+
+def test_encode_matches_reference_fixtures(tok, golden):
+    for e in golden["encode"]:
+        assert tok.encode(e["text"]) == e["ids"], e["text"][:60]
+
+
+def test_encode_bos_eos_flags(tok):
+    ids = tok.encode("Hello world", bos=False, eos=True)
+    assert ids[-1] == 2 and ids[0] != 1
+    assert tok.encode("", bos=False) == []
+
+
+def test_decode_matches_reference_fixtures(tok, golden):
+    for d in golden["decode"]:
+        assert tok.decode(d["prev"], d["token"]).hex() == d["hex"], d
+        assert int(tok.is_safe(d["prev"], d["token"])) == d["safe"], d
+
+
+def test_sampler_matches_reference_fixtures(host, golden):
+    for s in golden["sample"]:
+        r = np.random.default_rng(s["rng_seed"])
+        smp = host.Sampler(V, s["temperature"], s["topp"], s["seed"])
+        got = []
+        for _ in range(len(s["tokens"])):
+            lg = (r.standard_normal(V) * s["scale"]).astype(np.float32)
+            lg[r.integers(0, V, 40)] = lg.max()
+            got.append(smp.sample(lg))
+        assert got == s["tokens"], s
+        assert str(smp.rng) == s["final_rng"]
+
+
+def test_encode_fuzz_vs_live_reference(tok, ref):
+    L, t = ref
+    import make_host_golden as M
+    rng = np.random.default_rng(7)
+    alphabet = list("abcdefghijklmnopqrstuvwxyz ABCDEFGHIJKLMNOPQRSTUVWXYZ.,;:!?'\"\n\t0123456789") + \
+        ["é", "ü", "ß", "日", "本", "😀", "🎉", "Ω", "ñ", "​", "ő"]
+    for n in range(300):
+        s = "".join(rng.choice(alphabet, int(rng.integers(0, 80))))
+        assert tok.encode(s) == M.encode(L, t, s), repr(s)
+    # raw bytes, invalid UTF-8 included
+    for n in range(200):
+        raw = bytes(rng.integers(1, 256, int(rng.integers(0, 40))).astype(np.uint8))
+        assert tok.encode(raw) == M.encode(L, t, raw), raw
+
+
+def test_decode_every_token_vs_live_reference(tok, ref):
+    L, t = ref
+    for prev in (1, 13, 29871):
+        for tk in range(V):
+            p = L.ref_tok_decode(t, prev, tk)
+            assert tok.decode(prev, tk) == C.string_at(p), (prev, tk)
+            assert int(tok.is_safe(prev, tk)) == L.ref_piece_safe(p), (prev, tk)
+
+
+def test_sampler_vs_live_reference(host, ref):
+    L, _ = ref
+    rng = np.random.default_rng(11)
+    for trial in range(30):
+        temp = float(rng.choice([0.0, 0.5, 1.0, 1.5]))
+        topp = float(rng.choice([0.0, 0.3, 0.9, 0.99, 1.0]))
+        seed = int(rng.integers(1, 2**40))
+        ours = host.Sampler(V, temp, topp, seed)
+        theirs = L.ref_sampler_new(V, temp, topp, seed)
+        for step in range(8):
+            lg = (rng.standard_normal(V) * float(rng.choice([0.01, 1.0, 5.0, 20.0]))).astype(np.float32)
+            if step % 3 == 0:
+                lg[rng.integers(0, V, 500)] = lg[0]  # many exact ties
+            a, b = lg.copy(), lg.copy()
+            assert ours.sample(a) == L.ref_sample(theirs, b.ctypes.data_as(C.POINTER(C.c_float)))
+            np.testing.assert_array_equal(a, b)  # same in-place softmax
+            assert ours.rng == L.ref_sampler_rng(theirs)
+        L.ref_sampler_free(theirs)
+
+
+def test_requests_roundtrip(host, tmp_path):
+    src = os.path.join(GOLD, "gen_in_8.txt")
+    r = host.Requests(src, 27, 1024)
+    assert len(r) == 8
+    lines = open(src, "rb").read().split(b"\n")
+    for i in range(8):
+        assert r.prompt(i) == lines[1 + i]
+    out = tmp_path / "out.txt"
+    r.write(str(out))
+    assert out.read_bytes() == b"8\n" + b"\n" * 8
+
+
+def _fake_logits(token, pos):
+    """Deterministic logits per (token, pos): peaked enough that generations differ by prompt,
+    with EOS growing likelier with position so sequences end at varied lengths."""
+    r = np.random.default_rng(int(token) * 100003 + int(pos))
+    lg = (r.standard_normal(V) * 2.5).astype(np.float32)
+    lg[2] = np.float32(-4.0 + 0.25 * pos)
+    return lg
+
+
+def _expected_outputs(host, tok, prompts, seq_len):
+    """Per-request restatement of test_data_parallelism (src/llama.cpp:1021-1067): each request
+    is independent of the batch it shares, so its output is a plain sequential generation."""
+    outs, gen = [], 0
+    for p in prompts:
+        ids = tok.encode(p)
+        smp = host.Sampler(V, 1.0, 0.9, 314028)
+        token, pos, text = ids[0], 0, b""
+        while True:
+            lg = _fake_logits(token, pos)
+            nxt = ids[pos + 1] if pos < len(ids) - 1 else smp.sample(lg)
+            pos += 1
+            if nxt in (1, 2):
+                break
+            if tok.is_safe(token, nxt):
+                text += tok.decode(token, nxt)
+            token = nxt
+            if pos >= seq_len:
+                break
+        outs.append(text + b"\n")
+        gen += pos - 1
+    return outs, gen
+
+
+@pytest.mark.parametrize("workers,batch", [(1, 1), (1, 3), (2, 2), (3, 5)])
+def test_scheduler_outputs_independent_of_placement(host, tok, tmp_path, workers, batch):
+    src = tmp_path / "in.txt"
+    prompts = ["Once upon a time", "The serene landscape", "", "héllo", "A brief message:", "x" * 40, "Why?"]
+    src.write_bytes((f"{len(prompts)}\n" + "\n".join(prompts) + "\n").encode())
+    seq_len = 48
+    r = host.Requests(str(src), 27, seq_len)
+
+    def step(worker, toks, pos):
+        return np.stack([_fake_logits(t, p) for t, p in zip(toks, pos)])
+    gen = r.serve(TOK, V, workers, batch, step)
+    want, want_gen = _expected_outputs(host, tok, [p.encode() for p in prompts], seq_len)
+    assert [r.output(i) for i in range(len(prompts))] == want
+    assert gen == want_gen
+    out = tmp_path / "out.txt"
+    r.write(str(out))
+    assert out.read_bytes() == f"{len(prompts)}\n".encode() + b"".join(w + b"\n" for w in want)
