@@ -4,7 +4,8 @@
 //                   [-m generate|chat|test] [-y system] [-f input] [-o output] [-b batch]
 //
 // Same flags, defaults, validation and output files.  What differs is underneath:
-//  * the model is read once (mmap, src/utils.cpp:150-170 semantics), uploaded to GPU 0 with
+//  * the model — a v0 fp32 model.bin, or a runq v2 "ak42" int8 file (the int8 decoder) — is
+//    read once (mmap, src/utils.cpp:150-170 / runq.c:219-251 semantics), uploaded to GPU 0 with
 //    ONE copy and replicated to every other GPU with an RCCL broadcast over xGMI (the
 //    reference uploads the full model from host memory once per GPU thread);
 //  * every decode step is the fused decoder of libthallama.so (the persistent one-launch step
@@ -25,6 +26,7 @@
 #include "../../include/models.hpp"
 #include "../../include/thallama.h"
 #include "../../include/thallama_host.h"
+#include "../../include/thaQ8.hpp"
 
 #define HIP_OK(cmd)                                                                              \
   do {                                                                                           \
@@ -68,27 +70,78 @@ static void error_usage() {
   exit(EXIT_FAILURE);
 }
 
-// One GPU's replica: weights (an arena view), run state for `batch` sequences, the decoder.
+// The model file: a llama2.c v0 fp32 checkpoint (src/utils.cpp:150-170) or a runq v2 "ak42"
+// int8 checkpoint (runq.c:219-251), told apart by the v2 magic.
+struct ModelFile {
+  bool q8 = false;
+  Transformer t{};     // v0: mmapped fp32 model (build_transformer)
+  Q8Checkpoint ck{};   // v2: mmapped int8 payload
+  Config cfg{};
+  const void* payload = nullptr;  // host image of the device arena
+  size_t bytes = 0;
+};
+
+static void open_model(ModelFile& m, char* path) {
+  FILE* f = fopen(path, "rb");
+  if (!f) {
+    fprintf(stderr, "Couldn't open file %s\n", path);
+    exit(EXIT_FAILURE);
+  }
+  uint32_t magic = 0;
+  const bool got = fread(&magic, 4, 1, f) == 1;
+  fclose(f);
+  if (got && magic == 0x616b3432u) {
+    const int r = thallama_q8_read_checkpoint(path, &m.ck);
+    if (r != 0) {
+      fprintf(stderr, "cannot read int8 checkpoint %s (%d)\n", path, r);
+      exit(EXIT_FAILURE);
+    }
+    m.q8 = true;
+    m.cfg = m.ck.config;
+    m.payload = m.ck.payload;
+    m.bytes = thallama_q8_payload_bytes(&m.cfg, m.ck.shared_classifier, m.ck.group_size);
+    m.t.config = m.cfg;
+    printf("---------Model Information----------\n");
+    printf("int8 (runq v2) group_size: %d\n", m.ck.group_size);
+    printf("dim: %d\nhidden_dim: %d\nn_layers: %d\nn_heads: %d\nn_kv_heads: %d\nvocab_size: %d\nseq_len: %d\n",
+           m.cfg.dim, m.cfg.hidden_dim, m.cfg.n_layers, m.cfg.n_heads, m.cfg.n_kv_heads, m.cfg.vocab_size,
+           m.cfg.seq_len);
+    printf("------------------------------------\n");
+  } else {
+    build_transformer(&m.t, path);
+    m.cfg = m.t.config;
+    const int shared = m.t.weights.wcls == m.t.weights.token_embedding_table;
+    m.payload = m.t.weights.token_embedding_table;
+    m.bytes = thallama_v0_payload_floats(&m.cfg, shared) * sizeof(float);
+  }
+}
+
+static void close_model(ModelFile& m) {
+  if (m.q8) thallama_q8_close_checkpoint(&m.ck);
+  else free_transformer(&m.t);
+}
+
+// One GPU's replica: the weight arena, run state for `batch` sequences, the decoder.
 struct Replica {
   int dev = 0;
+  void* arena = nullptr;
   TransformerWeights w{};
+  Q8TransformerWeights w8{};
+  float* emb = nullptr;  // int8: dequantised embedding
   RunState* s = nullptr;
   thallama_decoder* dec = nullptr;
 };
 
 // Weights on every device: one H2D copy to device 0, then an RCCL broadcast (in 1 GiB
-// pieces) into every other device's arena.  Returns the per-device weight views.
-static std::vector<Replica> replicate(Transformer* t, int n_dev, int batch) {
-  const int shared = t->weights.wcls == t->weights.token_embedding_table;
-  const size_t n = thallama_v0_payload_floats(&t->config, shared);
+// pieces) into every other device's arena.
+static std::vector<Replica> replicate(ModelFile& m, int n_dev, int batch) {
   std::vector<Replica> reps((size_t)n_dev);
-  std::vector<float*> arena((size_t)n_dev, nullptr);
   for (int d = 0; d < n_dev; ++d) {
     HIP_OK(hipSetDevice(d));
-    HIP_OK(hipMalloc(&arena[d], n * sizeof(float)));
+    HIP_OK(hipMalloc(&reps[d].arena, m.bytes));
   }
   HIP_OK(hipSetDevice(0));
-  HIP_OK(hipMemcpy(arena[0], t->weights.token_embedding_table, n * sizeof(float), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(reps[0].arena, m.payload, m.bytes, hipMemcpyHostToDevice));
   if (n_dev > 1) {
     std::vector<ncclComm_t> comms((size_t)n_dev);
     std::vector<int> devs((size_t)n_dev);
@@ -99,12 +152,13 @@ static std::vector<Replica> replicate(Transformer* t, int n_dev, int batch) {
       HIP_OK(hipSetDevice(d));
       HIP_OK(hipStreamCreate(&st[d]));
     }
-    const size_t piece = (size_t)1 << 28;  // floats (1 GiB)
-    for (size_t off = 0; off < n; off += piece) {
-      const size_t cnt = n - off < piece ? n - off : piece;
+    const size_t piece = (size_t)1 << 30;  // bytes
+    for (size_t off = 0; off < m.bytes; off += piece) {
+      const size_t cnt = m.bytes - off < piece ? m.bytes - off : piece;
       NCCL_OK(ncclGroupStart());
       for (int d = 0; d < n_dev; ++d)
-        NCCL_OK(ncclBroadcast(arena[0] + off, arena[d] + off, cnt, ncclFloat, 0, comms[d], st[d]));
+        NCCL_OK(ncclBroadcast((char*)reps[0].arena + off, (char*)reps[d].arena + off, cnt, ncclChar, 0, comms[d],
+                              st[d]));
       NCCL_OK(ncclGroupEnd());
     }
     for (int d = 0; d < n_dev; ++d) {
@@ -118,9 +172,23 @@ static std::vector<Replica> replicate(Transformer* t, int n_dev, int batch) {
     HIP_OK(hipSetDevice(d));
     Replica& r = reps[d];
     r.dev = d;
-    thallama_map_weights(&r.w, &t->config, arena[d], shared);
-    alloc_state_to_device_batch(t, &r.s, batch);
-    if (thallama_decoder_create(&r.dec, &t->config, &r.w, r.s, batch, nullptr) != 0) {
+    alloc_state_to_device_batch(&m.t, &r.s, batch);
+    int rc;
+    if (m.q8) {
+      HIP_OK(hipMalloc(&r.emb, sizeof(float) * (size_t)m.cfg.vocab_size * m.cfg.dim));
+      if (thallama_q8_map(&r.w8, &m.cfg, r.arena, m.ck.shared_classifier, m.ck.group_size, r.emb) != 0 ||
+          thallama_q8_dequant_embedding(&r.w8, &m.cfg, nullptr) != 0) {
+        fprintf(stderr, "int8 weights on device %d: %s\n", d, thallama_last_error());
+        exit(EXIT_FAILURE);
+      }
+      HIP_OK(hipDeviceSynchronize());
+      rc = thallama_decoder_create_q8(&r.dec, &m.cfg, &r.w8, r.s, batch, nullptr);
+    } else {
+      const int shared = m.t.weights.wcls == m.t.weights.token_embedding_table;
+      thallama_map_weights(&r.w, &m.cfg, (float*)r.arena, shared);
+      rc = thallama_decoder_create(&r.dec, &m.cfg, &r.w, r.s, batch, nullptr);
+    }
+    if (rc != 0) {
       fprintf(stderr, "decoder on device %d: %s\n", d, thallama_last_error());
       exit(EXIT_FAILURE);
     }
@@ -133,7 +201,11 @@ static void release(std::vector<Replica>& reps) {
     HIP_OK(hipSetDevice(r.dev));
     thallama_decoder_destroy(r.dec);
     free_state_device(r.s);
-    HIP_OK(hipFree(r.w.token_embedding_table));
+    if (r.emb) {
+      thallama_q8_unmap(&r.w8);
+      HIP_OK(hipFree(r.emb));
+    }
+    HIP_OK(hipFree(r.arena));
   }
 }
 
@@ -148,7 +220,7 @@ static int replica_step(void* ctx, int worker, int batch, const int* token, cons
 }
 
 // generate mode (src/llama.cpp:522-579), on GPU 0
-static void generate(Transformer* t, Replica& r, thallama_tokenizer* tok, thallama_sampler* smp, const char* prompt,
+static void generate(const Config& cfg, Replica& r, thallama_tokenizer* tok, thallama_sampler* smp, const char* prompt,
                      int steps) {
   if (!prompt) prompt = "";
   std::vector<int> ids(strlen(prompt) + 3);
@@ -158,7 +230,7 @@ static void generate(Transformer* t, Replica& r, thallama_tokenizer* tok, thalla
     fprintf(stderr, "something is wrong, expected at least 1 prompt token\n");
     exit(EXIT_FAILURE);
   }
-  std::vector<float> logits((size_t)t->config.vocab_size);
+  std::vector<float> logits((size_t)cfg.vocab_size);
   long start = 0;
   int token = ids[0], pos = 0;
   while (pos < steps) {
@@ -220,10 +292,10 @@ int main(int argc, char* argv[]) {
   if (steps < 0) steps = 0;
   if (batch < 1) batch = 1;
 
-  Transformer transformer;
-  build_transformer(&transformer, checkpoint_path);
-  if (steps == 0 || steps > transformer.config.seq_len) steps = transformer.config.seq_len;
-  const int V = transformer.config.vocab_size;
+  ModelFile model;
+  open_model(model, checkpoint_path);
+  if (steps == 0 || steps > model.cfg.seq_len) steps = model.cfg.seq_len;
+  const int V = model.cfg.vocab_size;
   thallama_tokenizer* tok = thallama_tokenizer_load(tokenizer_path, V);
   if (!tok) {
     fprintf(stderr, "couldn't load %s\n", tokenizer_path);
@@ -232,13 +304,13 @@ int main(int argc, char* argv[]) {
   thallama_sampler* smp = thallama_sampler_create(V, temperature, topp, rng_seed);
 
   if (strcmp(mode, "generate") == 0) {
-    std::vector<Replica> reps = replicate(&transformer, 1, 1);
-    generate(&transformer, reps[0], tok, smp, prompt, steps);
+    std::vector<Replica> reps = replicate(model, 1, 1);
+    generate(model.cfg, reps[0], tok, smp, prompt, steps);
     release(reps);
   } else if (strcmp(mode, "chat") == 0) {
     // chat() is commented out in the reference's main (src/llama.cpp:1590)
   } else if (strcmp(mode, "test") == 0) {
-    steps = transformer.config.seq_len;
+    steps = model.cfg.seq_len;
     if (!input_filename || !output_filename) error_usage();
     const int max_token_len = thallama_tokenizer_max_token_length(tok);
     printf("max_token_len: %d, max_seq_len: %d\n", max_token_len, steps);
@@ -255,7 +327,7 @@ int main(int argc, char* argv[]) {
     fprintf(stderr, "\n Num Devices %d\n", n_dev);
     fprintf(stderr, "\n Batch Size %d\n", batch);
     const long load_start = time_in_ms();
-    std::vector<Replica> reps = replicate(&transformer, n_dev, batch);
+    std::vector<Replica> reps = replicate(model, n_dev, batch);
     fprintf(stdout, "\nLoad model time (1 upload + RCCL broadcast to %d GPUs): %f\n", n_dev,
             (double)(time_in_ms() - load_start) / 1000);
 
@@ -282,7 +354,7 @@ int main(int argc, char* argv[]) {
   }
   thallama_sampler_free(smp);
   thallama_tokenizer_free(tok);
-  free_transformer(&transformer);
+  close_model(model);
   fprintf(stdout, "total elapsed time(s): %lf\n", (double)(time_in_ms() - total_start) / 1000);
   return 0;
 }

@@ -1,8 +1,11 @@
 // q8.hip — int8 (Q8_0, runq layout) entry points: launcher of gemv_q8.hpp, activation /
 // weight quantisation kernels, v2 payload mapping (include/thaQ8.hpp).
+#include <fcntl.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <unistd.h>
 #include "../../include/thaQ8.hpp"
 #include "../../include/hip_helper.hpp"
 #include "gemv_q8.hpp"
@@ -307,4 +310,55 @@ extern "C" int thallama_q8_quantize_model(void* payload, const TransformerWeight
       ptr += t.each + 4 * ng;
     }
   return 0;
+}
+
+// ---------------------------------------------------------------- v2 checkpoint (host)
+// runq.c read_checkpoint (:219-251): magic 0x616b3432 "ak42", version 2, Config, one flag
+// byte (shared classifier), int group size, payload at byte 256.  Errors are returned, not
+// exit()ed, so a library caller can recover.
+extern "C" int thallama_q8_read_checkpoint(const char* path, Q8Checkpoint* ck) {
+  if (!path || !ck) return -1;
+  memset(ck, 0, sizeof(*ck));
+  ck->fd = -1;
+  FILE* f = fopen(path, "rb");
+  if (!f) return -1;
+  uint32_t magic = 0;
+  int version = 0;
+  uint8_t shared = 0;
+  int gs = 0;
+  const bool ok = fread(&magic, 4, 1, f) == 1 && fread(&version, 4, 1, f) == 1 &&
+                  fread(&ck->config, sizeof(Config), 1, f) == 1 && fread(&shared, 1, 1, f) == 1 &&
+                  fread(&gs, 4, 1, f) == 1;
+  fseek(f, 0, SEEK_END);
+  const long size = ftell(f);
+  fclose(f);
+  if (!ok) return -1;
+  if (magic != 0x616b3432u) return -2;
+  if (version != 2) return -3;
+  ck->shared_classifier = shared;
+  ck->group_size = gs;
+  if (size < 256 || gs <= 0 ||
+      (size_t)(size - 256) < thallama_q8_payload_bytes(&ck->config, shared, gs))
+    return -4;
+  ck->fd = open(path, O_RDONLY);
+  if (ck->fd < 0) return -1;
+  void* m = mmap(nullptr, (size_t)size, PROT_READ, MAP_PRIVATE, ck->fd, 0);
+  if (m == MAP_FAILED) {
+    close(ck->fd);
+    ck->fd = -1;
+    return -1;
+  }
+  ck->data = m;
+  ck->file_size = (size_t)size;
+  ck->payload = (const char*)m + 256;
+  ck->payload_bytes = (size_t)size - 256;
+  return 0;
+}
+
+extern "C" void thallama_q8_close_checkpoint(Q8Checkpoint* ck) {
+  if (!ck) return;
+  if (ck->data) munmap(ck->data, ck->file_size);
+  if (ck->fd >= 0) close(ck->fd);
+  ck->data = nullptr;
+  ck->fd = -1;
 }

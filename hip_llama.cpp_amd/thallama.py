@@ -72,6 +72,13 @@ class Q8TransformerWeights(C.Structure):
                [("rms_final_weight", c_float_p), ("wcls", C.POINTER(QuantizedTensor)), ("group_size", C.c_int)]
 
 
+class Q8Checkpoint(C.Structure):
+    """include/thaQ8.hpp: a v2 "ak42" file opened like runq.c read_checkpoint (:219-251)"""
+    _fields_ = [("config", Config), ("shared_classifier", C.c_int), ("group_size", C.c_int), ("fd", C.c_int),
+                ("data", C.c_void_p), ("file_size", C.c_size_t), ("payload", C.c_void_p),
+                ("payload_bytes", C.c_size_t)]
+
+
 class Handle(C.Structure):
     """thablasHandle_t, reference include/thaBLAS.hpp:21-25"""
     _fields_ = [("current_gpu_id", C.c_int), ("calc_stream", C.c_void_p), ("copy_stream", C.c_void_p)]
@@ -132,6 +139,10 @@ def lib():
             "thallama_decoder_create_q8": (I, [C.POINTER(VP), C.POINTER(Config), C.POINTER(Q8TransformerWeights),
                                                C.POINTER(RunState), I, VP]),
             "thallama_q8_payload_bytes": (S, [C.POINTER(Config), I, I]),
+            "thallama_q8_read_checkpoint": (I, [C.c_char_p, C.POINTER(Q8Checkpoint)]),
+            "thallama_q8_close_checkpoint": (None, [C.POINTER(Q8Checkpoint)]),
+            "read_checkpoint": (None, [C.c_char_p, C.POINTER(Config), C.POINTER(TransformerWeights),
+                                       C.POINTER(C.c_int), C.POINTER(P), C.POINTER(C.c_ssize_t)]),
             "thallama_q8_map": (I, [C.POINTER(Q8TransformerWeights), C.POINTER(Config), VP, I, I, P]),
             "thallama_q8_unmap": (None, [C.POINTER(Q8TransformerWeights)]),
             "thallama_q8_dequant_embedding": (I, [C.POINTER(Q8TransformerWeights), C.POINTER(Config), VP]),

@@ -48,6 +48,22 @@ int thallama_q8_map(Q8TransformerWeights* w, const Config* p, void* payload_dev,
                     int group_size, float* emb_f32);
 void thallama_q8_unmap(Q8TransformerWeights* w);
 
+// A v2 ("ak42") checkpoint opened like runq.c read_checkpoint (:219-251): the 256-byte header
+// parsed, the file mmapped read-only, `payload` pointing just past the header (host memory).
+typedef struct {
+  Config config;           // vocab_size as stored (positive)
+  int shared_classifier;   // header flag byte
+  int group_size;          // GS
+  int fd;
+  void* data;              // the whole mapping
+  size_t file_size;
+  const void* payload;     // data + 256
+  size_t payload_bytes;    // file_size - 256 (>= thallama_q8_payload_bytes)
+} Q8Checkpoint;
+// 0 on success; -1 unreadable, -2 bad magic, -3 bad version, -4 truncated payload.
+int thallama_q8_read_checkpoint(const char* path, Q8Checkpoint* ck);
+void thallama_q8_close_checkpoint(Q8Checkpoint* ck);
+
 // token_embedding_table[i] = q_tokens.q[i] * q_tokens.s[i / GS]  (runq.c:139-143)
 int thallama_q8_dequant_embedding(const Q8TransformerWeights* w, const Config* p, hipStream_t stream);
 

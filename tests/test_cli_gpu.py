@@ -111,3 +111,31 @@ def test_usage_errors(gpu, tmp_path):
     assert r.returncode != 0 and b"Usage:" in r.stderr
     r = subprocess.run([RUN, "x.bin", "-q", "1"], capture_output=True, timeout=60)
     assert r.returncode != 0 and b"Usage:" in r.stderr
+
+
+def test_generate_mode_int8_checkpoint(gpu, host, oracle, tmp_path):
+    """A runq v2 ("ak42") int8 file runs through the int8 decoder; greedy text identical to the
+    CPU oracle's runq.c restatement."""
+    base = oracle.Model(CFG, 0, seed=77)
+    arena = base.arena().copy()
+    arena[-V * CFG[0]:] *= 30.0
+    ref = oracle.Model(CFG, 0, payload=arena)
+    ref.build_q8(64)
+    path = str(tmp_path / "model_q8.bin")
+    ref.write_v2(path)
+    prompt = "The serene landscape"
+    r = run_cli([path, "-t", "0", "-n", "32", "-i", prompt, "-z", TOK], tmp_path)
+    assert b"int8 (runq v2) group_size: 64" in r.stdout
+    tok = host.Tokenizer(TOK, V)
+    ids = tok.encode(prompt)
+    token, pos, text = ids[0], 0, b""
+    while pos < 32:
+        lg = ref.q8_forward(token, pos)
+        nxt = ids[pos + 1] if pos < len(ids) - 1 else int(np.argmax(lg))
+        pos += 1
+        if nxt == 1:
+            break
+        if tok.is_safe(token, nxt):
+            text += tok.decode(token, nxt)
+        token = nxt
+    assert r.stdout.split(b"------------------------------------\n")[-1].startswith(text + b"\n")
