@@ -31,6 +31,7 @@
 #include "gemv_dispatch.hpp"
 #include "q8_dispatch.hpp"
 #include "persist.hpp"
+#include "prefill.hpp"
 
 using tl::f4;
 
@@ -122,6 +123,7 @@ struct thallama_decoder {
   int* tok_h = nullptr;  // pinned staging
   int* pos_h = nullptr;
   float2* rope_d = nullptr;
+  float* xn_d = nullptr;        // [<=16][dim] normed rows for the matrix-core GEMV (batch >= 2)
   float* part_d = nullptr;      // attention partials [B][H][<=16 units][hs+4]
   unsigned* cnt_d = nullptr;    // attention combine tickets [B][H]
   bool q8 = false;              // int8 (runq Q8_0) weights in w8; w then holds only norms + embedding
@@ -141,6 +143,11 @@ struct thallama_decoder {
   bool pok = false;             // shape supported
   unsigned long long* ptrace = nullptr;  // optional timeline of the persistent step
   size_t ptrace_n = 0;
+  // batched prompt processing (prefill.hip), allocated on first use for kPrefillChunk tokens
+  float *pf_x = nullptr, *pf_xn = nullptr, *pf_q = nullptr, *pf_xb = nullptr, *pf_hb = nullptr;
+  float* pf_part = nullptr;
+  unsigned* pf_cnt = nullptr;
+  int *pf_tok = nullptr, *pf_pos = nullptr;
   std::string pwhy;             // why not
   // profiling
   std::vector<hipEvent_t> ev_pool;
@@ -246,6 +253,7 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
   TL_TRY(hipMalloc(&d->rope_d, rope.size() * sizeof(float2)));
   TL_TRY(hipMemcpy(d->rope_d, rope.data(), rope.size() * sizeof(float2), hipMemcpyHostToDevice));
   d->nsplit = auto_splits(d);
+  if (batch >= 2) TL_TRY(hipMalloc(&d->xn_d, sizeof(float) * (size_t)(batch < 16 ? batch : 16) * d->dim));
   {
     const size_t nsmax = (size_t)((d->S + kAttnChunk - 1) / kAttnChunk);
     const size_t recs = (size_t)batch * d->H * (nsmax > 16 ? nsmax : 16);
@@ -292,12 +300,16 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   (void)hipHostFree(d->tok_h);
   (void)hipHostFree(d->pos_h);
   (void)hipFree(d->rope_d);
+  (void)hipFree(d->xn_d);
   (void)hipFree(d->part_d);
   (void)hipFree(d->cnt_d);
   (void)hipFree(d->psync);
   (void)hipFree(d->pbmax);
   (void)hipFree(d->pgran);
   (void)hipFree(d->ptrace);
+  for (void* b : {(void*)d->pf_x, (void*)d->pf_xn, (void*)d->pf_q, (void*)d->pf_xb, (void*)d->pf_hb,
+                  (void*)d->pf_part, (void*)d->pf_cnt, (void*)d->pf_tok, (void*)d->pf_pos})
+    (void)hipFree(b);
   if (d->own_stream) (void)hipStreamDestroy(d->stream);
   delete d;
 }
@@ -357,6 +369,7 @@ static int enqueue_step(thallama_decoder* d) {
       p.x = s.x;
       p.x_stride = dim;
       p.rms_w = w.rms_att_weight + ll * dim;
+      p.xn = d->xn_d;
       if (l == 0) {
         p.tok = d->tok_d;
         p.emb = w.token_embedding_table;
@@ -463,6 +476,7 @@ static int enqueue_step(thallama_decoder* d) {
       p.x = s.x;
       p.x_stride = dim;
       p.rms_w = w.rms_ffn_weight + ll * dim;
+      p.xn = d->xn_d;
       p.y = s.hb;
       p.y_stride = hid;
       int ev = prof_begin(d);
@@ -495,6 +509,7 @@ static int enqueue_step(thallama_decoder* d) {
     p.x = s.x;
     p.x_stride = dim;
     p.rms_w = w.rms_final_weight;
+    p.xn = d->xn_d;
     if (d->L == 0) {
       p.tok = d->tok_d;
       p.emb = w.token_embedding_table;
@@ -818,4 +833,101 @@ extern "C" thablasStatus_t thaDNN_q8_forward_batch(thablasHandle_t handle, int n
     return r == (int)hipErrorInvalidValue ? THABLAS_STATUS_INVALID_VALUE : THABLAS_STATUS_EXECUTION_FAILED;
   }
   return THABLAS_STATUS_SUCCESS;
+}
+
+// ------------------------------------------------------------------ batched prefill
+// Prompt tokens go through each layer together (prefill.hip): one fp32-MFMA GEMM per
+// projection for up to kPrefillChunk tokens, the decode attention kernel over the chunk's
+// positions, K/V rows written at pos0.. of sequence b.  No logits: the caller's next decode
+// step starts from the token after the prefilled ones.  fp32 weights, head size 64/128/256.
+static constexpr int kPrefillChunk = 128;
+
+extern "C" int thallama_decoder_prefill(thallama_decoder* d, int b, const int* tokens_h, int n, int pos0) {
+  if (!d || !tokens_h || n < 0 || b < 0 || b >= d->B || pos0 < 0 || pos0 + n > d->S) {
+    g_last_error = "thallama_decoder_prefill: invalid argument";
+    return (int)hipErrorInvalidValue;
+  }
+  if (n == 0) return 0;
+  if (d->q8 || (d->hs != 64 && d->hs != 128 && d->hs != 256) || d->dim % 32 || d->hidden % 32) {
+    g_last_error = "thallama_decoder_prefill: unsupported (int8 weights, or head size not 64/128/256)";
+    return (int)hipErrorNotSupported;
+  }
+  for (int i = 0; i < n; ++i)
+    if (tokens_h[i] < 0 || tokens_h[i] >= d->V) {
+      g_last_error = "thallama_decoder_prefill: token out of range";
+      return (int)hipErrorInvalidValue;
+    }
+  const int CH = kPrefillChunk, dim = d->dim, hid = d->hidden, kvd = d->kv_dim, S = d->S;
+  const int max_ns = 16;
+  if (!d->pf_x) {
+    TL_TRY(hipMalloc(&d->pf_x, sizeof(float) * (size_t)CH * dim));
+    TL_TRY(hipMalloc(&d->pf_xn, sizeof(float) * (size_t)CH * (dim > hid ? dim : hid)));
+    TL_TRY(hipMalloc(&d->pf_q, sizeof(float) * (size_t)CH * dim));
+    TL_TRY(hipMalloc(&d->pf_xb, sizeof(float) * (size_t)CH * dim));
+    TL_TRY(hipMalloc(&d->pf_hb, sizeof(float) * (size_t)CH * hid));
+    TL_TRY(hipMalloc(&d->pf_part, sizeof(float) * (size_t)CH * d->H * max_ns * (d->hs + 4)));
+    TL_TRY(hipMalloc(&d->pf_cnt, sizeof(unsigned) * (size_t)CH * d->H));
+    TL_TRY(hipMemset(d->pf_cnt, 0, sizeof(unsigned) * (size_t)CH * d->H));
+    TL_TRY(hipMalloc(&d->pf_tok, sizeof(int) * CH));
+    TL_TRY(hipMalloc(&d->pf_pos, sizeof(int) * CH));
+  }
+  const TransformerWeights& w = d->w;
+  const long long kv_b_stride = (long long)d->L * S * kvd;
+  float* kc_b = d->s.key_cache + (long long)b * kv_b_stride;
+  float* vc_b = d->s.value_cache + (long long)b * kv_b_stride;
+  hipStream_t st = d->stream;
+  for (int c = 0; c < n; c += CH) {
+    const int m = n - c < CH ? n - c : CH;
+    const int p0 = pos0 + c;
+    TL_TRY(hipMemcpyAsync(d->pf_tok, tokens_h + c, sizeof(int) * m, hipMemcpyHostToDevice, st));
+    TL_TRY(tl::prefill_positions(d->pf_pos, p0, m, st));
+    TL_TRY(tl::prefill_embed(d->pf_x, w.token_embedding_table, d->pf_tok, m, dim, st));
+    for (int l = 0; l < d->L; ++l) {
+      const long long ll = l;
+      tl::PGemmArgs g = {};
+      g.n = m;
+      g.dim = dim; g.kv_dim = kvd; g.head_size = d->hs; g.rope = d->rope_d; g.pos0 = p0;
+      // RMSNorm + QKV + RoPE + K/V rows
+      TL_TRY(tl::prefill_rmsnorm(d->pf_xn, d->pf_x, w.rms_att_weight + ll * dim, m, dim, st));
+      g.X = d->pf_xn; g.ldx = dim; g.K = dim; g.M = dim + 2 * kvd;
+      g.W0 = w.wq + ll * dim * dim; g.W1 = w.wk + ll * dim * kvd; g.W2 = w.wv + ll * dim * kvd;
+      g.Y = d->pf_q; g.ldy = dim;
+      g.kc = kc_b + ll * S * kvd; g.vc = vc_b + ll * S * kvd;
+      TL_TRY(tl::prefill_gemm(tl::GM_QKV, g, st));
+      // causal attention: the chunk's m positions as "sequences" over this sequence's cache
+      {
+        tl::AttnWaveParams wp = {};
+        tl::AttnParams& a = wp.a;
+        a.q = d->pf_q; a.kc = kc_b; a.vc = vc_b; a.kv_b_stride = 0; a.kv_l_off = ll * S * kvd;
+        a.pos = d->pf_pos; a.out = d->pf_xb; a.part = d->pf_part;
+        a.dim = dim; a.kv_dim = kvd; a.head_size = d->hs; a.n_heads = d->H; a.kv_mul = d->kv_mul;
+        a.seq_len = S; a.nsplit = 1; a.min_chunk = 32;
+        wp.cnt = d->pf_cnt; wp.B = m;
+        int ns = (256 + m * d->H - 1) / (m * d->H);
+        ns = ns < 1 ? 1 : (ns > max_ns ? max_ns : ns);
+        wp.NS = ns;
+        const int units = m * d->H * ns;
+        if (d->hs == 64)
+          hipLaunchKernelGGL((tl::attn_wave_kernel<64, kAttnChunk>), dim3(units), dim3(64), 0, st, wp);
+        else if (d->hs == 128)
+          hipLaunchKernelGGL((tl::attn_wave_kernel<128, kAttnChunk>), dim3(units), dim3(64), 0, st, wp);
+        else
+          hipLaunchKernelGGL((tl::attn_wave_kernel<256, kAttnChunk / 2>), dim3(units), dim3(64), 0, st, wp);
+        TL_TRY(hipGetLastError());
+      }
+      // Wo + residual
+      g.X = d->pf_xb; g.ldx = dim; g.K = dim; g.M = dim; g.W0 = w.wo + ll * dim * dim; g.Y = d->pf_x; g.ldy = dim;
+      TL_TRY(tl::prefill_gemm(tl::GM_RESID, g, st));
+      // RMSNorm + W1/W3 + SwiGLU
+      TL_TRY(tl::prefill_rmsnorm(d->pf_xn, d->pf_x, w.rms_ffn_weight + ll * dim, m, dim, st));
+      g.X = d->pf_xn; g.ldx = dim; g.K = dim; g.M = 2 * hid;
+      g.W0 = w.w1 + ll * dim * hid; g.W1 = w.w3 + ll * dim * hid; g.Y = d->pf_hb; g.ldy = hid;
+      TL_TRY(tl::prefill_gemm(tl::GM_SWIGLU, g, st));
+      // W2 + residual
+      g.X = d->pf_hb; g.ldx = hid; g.K = hid; g.M = dim; g.W0 = w.w2 + ll * dim * hid; g.Y = d->pf_x; g.ldy = dim;
+      TL_TRY(tl::prefill_gemm(tl::GM_RESID, g, st));
+    }
+  }
+  TL_TRY(hipStreamSynchronize(st));
+  return 0;
 }

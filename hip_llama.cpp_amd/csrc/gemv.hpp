@@ -63,6 +63,9 @@ struct GemvParams {
   const int8_t* Q0; const int8_t* Q1; const int8_t* Q2;
   const float* S0; const float* S1; const float* S2;
   int gs;
+  // optional scratch [nb][K] for the matrix-core path (gemv_mfma.hpp): when set, the
+  // RMSNorm / embedding prologue runs once per launch into it instead of once per block
+  float* xn;
 };
 
 TL_DEVICE float silu_mul(float a, float b) {

@@ -1,9 +1,21 @@
 // gemv_launch.hpp — launch templates of the streaming GEMV, instantiated one epilogue
 // mode per translation unit (gemv_m*.hip) so the variants compile in parallel.
 #pragma once
+#include <stdlib.h>
 #include "gemv_dispatch.hpp"
+#include "gemv_mfma.hpp"
 
 namespace tl {
+
+// Smallest batch that takes the matrix-core GEMV (env THALLAMA_MFMA_MIN_NB overrides; a
+// value above 16 disables it).
+inline int gemv_mfma_min_nb() {
+  static const int v = [] {
+    const char* e = getenv("THALLAMA_MFMA_MIN_NB");
+    return e ? atoi(e) : 4;
+  }();
+  return v;
+}
 
 template <int MODE, int NB, int IPW, bool NT, int WAVES, bool PF>
 inline void launch_one(const GemvParams& p, hipStream_t s, int kc, size_t lds) {
@@ -72,7 +84,24 @@ inline hipError_t launch_mode(const GemvParams& p0, hipStream_t s, const GemvCfg
     }
     const GemvCfg c = cfg ? *cfg : gemv_default_cfg(MODE, p.n_items, p.K, p.nb, nt);
     hipError_t e;
-    if (p.nb == 1) e = launch_nb<MODE, 1>(p, s, c);
+    if (!cfg && p.nb >= gemv_mfma_min_nb() && (p.K & 15) == 0 && (p.x_stride & 3) == 0 &&
+        ((!p.rms_w && !p.tok) || p.xn)) {
+      // several sequences: the matrix-core kernel (gemv_mfma.hpp); a norm / embedding
+      // prologue runs once into the scratch rows first
+      if (p.rms_w || p.tok) {
+        hipLaunchKernelGGL(gemv_prenorm_kernel, dim3(p.nb), dim3(256), 0, s, p);
+        p.x = p.xn;
+        p.x_stride = p.K;
+        p.rms_w = nullptr;
+        p.tok = nullptr;
+        p.x_out = nullptr;
+      }
+      const int rows = MODE == GM_QKV ? 2 * p.n_items : p.n_items;
+      const dim3 grid((rows + 15) / 16);
+      if (c.nt) hipLaunchKernelGGL((gemv_mfma_kernel<MODE, true>), grid, dim3(kMfmaWaves * 64), 0, s, p);
+      else hipLaunchKernelGGL((gemv_mfma_kernel<MODE, false>), grid, dim3(kMfmaWaves * 64), 0, s, p);
+      e = hipGetLastError();
+    } else if (p.nb == 1) e = launch_nb<MODE, 1>(p, s, c);
     else if (p.nb == 2) e = launch_nb<MODE, 2>(p, s, c);
     else if (p.nb <= 4) e = launch_nb<MODE, 4>(p, s, c);
     else if (p.nb <= 8) e = launch_nb<MODE, 8>(p, s, c);

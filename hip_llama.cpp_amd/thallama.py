@@ -154,6 +154,7 @@ def lib():
             "thallama_decoder_destroy": (None, [VP]),
             "thallama_decoder_set": (I, [VP, I, I]),
             "thallama_decoder_persistent": (I, [VP]),
+            "thallama_decoder_prefill": (I, [VP, I, c_int_p, I, I]),
             "thallama_decoder_ptrace": (I, [VP, I, C.POINTER(C.c_ulonglong), C.c_size_t]),
             "thallama_decoder_stream": (VP, [VP]),
             "thallama_decoder_forward": (I, [VP, c_int_p, c_int_p, P]),
@@ -387,6 +388,11 @@ class Decoder:
 
     def set(self, key, value):
         check(lib().thallama_decoder_set(self.h, key, int(value)), "decoder_set")
+
+    def prefill(self, b, tokens, pos0):
+        """Batched prompt processing for slot b (no logits; K/V rows at pos0..)."""
+        arr = (C.c_int * len(tokens))(*[int(t) for t in tokens])
+        return lib().thallama_decoder_prefill(self.h, b, arr, len(tokens), pos0)
 
     def persistent(self):
         """True if steps run as one persistent launch (persist.hip)."""

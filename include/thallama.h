@@ -78,6 +78,14 @@ int thallama_decoder_forward(thallama_decoder* d, const int* token_h, const int*
 int thallama_decoder_greedy(thallama_decoder* d, const int* token0_h, const int* pos0_h, int n_steps,
                             int* tokens_out_h, int sync);
 
+/* Batched prompt processing for sequence slot b: the n tokens tokens_h[0..n) at positions
+ * pos0..pos0+n-1 go through every layer together (fp32-MFMA GEMMs; K/V rows written), with
+ * no logits — the next thallama_decoder_forward/greedy step continues from position pos0+n.
+ * Equivalent to n forced decode steps of that slot (src/llama.cpp:1029-1031) within the fp32
+ * tolerance.  Returns hipErrorNotSupported for int8 decoders or head sizes other than
+ * 64/128/256 (callers then feed the prompt token by token).  Synchronous. */
+int thallama_decoder_prefill(thallama_decoder* d, int b, const int* tokens_h, int n, int pos0);
+
 /* Copy the device logits of the last step into logits_h[batch*vocab] (synchronous). */
 int thallama_decoder_logits(thallama_decoder* d, float* logits_h);
 
