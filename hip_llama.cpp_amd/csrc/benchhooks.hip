@@ -30,6 +30,8 @@ extern "C" int thallama_gemv_bench(int mode, int M, int K, int nb, int ipw, int 
   if (ncopy > 64) ncopy = 64;
   float *W = nullptr, *x = nullptr, *rw = nullptr, *y = nullptr, *kc = nullptr, *vc = nullptr;
   int* pos = nullptr;
+  float *xn = nullptr, *mpart = nullptr;
+  unsigned* mcnt = nullptr;
   float2* rope = nullptr;
   hipStream_t s = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -51,6 +53,12 @@ extern "C" int thallama_gemv_bench(int mode, int M, int K, int nb, int ipw, int 
   hipLaunchKernelGGL(k_bench_fill, dim3(16), dim3(256), 0, s, rw, (size_t)K, 99u, 1.f / 32768.f);
   hipLaunchKernelGGL(k_bench_fill, dim3(16), dim3(256), 0, s, (float*)rope, (size_t)S * hs, 5u, 1.f / 32768.f);
   CK(hipMemsetAsync(pos, 0, nb * 4, s));
+  if (ipw == 0) {
+    CK(hipMalloc(&xn, (size_t)16 * K * 4));
+    CK(hipMalloc(&mpart, (size_t)tl::mfma_target_blocks() * 2 * 256 * 4));
+    CK(hipMalloc(&mcnt, (size_t)tl::mfma_target_blocks() * 4));
+    CK(hipMemsetAsync(mcnt, 0, (size_t)tl::mfma_target_blocks() * 4, s));
+  }
   {
     tl::GemvParams p = {};
     p.K = K;
@@ -70,6 +78,9 @@ extern "C" int thallama_gemv_bench(int mode, int M, int K, int nb, int ipw, int 
     p.kv_dim = K;
     p.head_size = hs;
     p.rope = rope;
+    p.xn = xn;
+    p.mpart = mpart;
+    p.mcnt = mcnt;
     tl::GemvCfg c;
     c.ipw = ipw;
     c.waves = waves;
@@ -80,6 +91,7 @@ extern "C" int thallama_gemv_bench(int mode, int M, int K, int nb, int ipw, int 
       p.W0 = base;
       p.W1 = mode == tl::GM_SWIGLU ? base + (size_t)M * K : base + (size_t)K * K;
       p.W2 = base + 2 * (size_t)K * K;
+      if (ipw == 0) return tl::launch_gemv(mode, p, s, c.nt);  // default dispatch (matrix cores at nb >= 4)
       return tl::launch_gemv_cfg(mode, p, s, c);
     };
     for (int i = 0; i < 8; ++i) CK(launch(i % ncopy));
@@ -95,6 +107,7 @@ done:
   (void)hipStreamSynchronize(s);
   (void)hipFree(W); (void)hipFree(x); (void)hipFree(rw); (void)hipFree(y); (void)hipFree(kc); (void)hipFree(vc);
   (void)hipFree(pos); (void)hipFree(rope);
+  (void)hipFree(xn); (void)hipFree(mpart); (void)hipFree(mcnt);
   (void)hipEventDestroy(e0); (void)hipEventDestroy(e1); (void)hipStreamDestroy(s);
 #undef CK
   return (int)err;

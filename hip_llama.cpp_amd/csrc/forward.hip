@@ -124,6 +124,8 @@ struct thallama_decoder {
   int* pos_h = nullptr;
   float2* rope_d = nullptr;
   float* xn_d = nullptr;        // [<=16][dim] normed rows for the matrix-core GEMV (batch >= 2)
+  float* mpart_d = nullptr;     // matrix-core GEMV split-K partial tiles
+  unsigned* mcnt_d = nullptr;   //   and their tickets
   float* part_d = nullptr;      // attention partials [B][H][<=16 units][hs+4]
   unsigned* cnt_d = nullptr;    // attention combine tickets [B][H]
   bool q8 = false;              // int8 (runq Q8_0) weights in w8; w then holds only norms + embedding
@@ -253,7 +255,13 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
   TL_TRY(hipMalloc(&d->rope_d, rope.size() * sizeof(float2)));
   TL_TRY(hipMemcpy(d->rope_d, rope.data(), rope.size() * sizeof(float2), hipMemcpyHostToDevice));
   d->nsplit = auto_splits(d);
-  if (batch >= 2) TL_TRY(hipMalloc(&d->xn_d, sizeof(float) * (size_t)(batch < 16 ? batch : 16) * d->dim));
+  if (batch >= 2) {
+    const size_t nblk = (size_t)tl::mfma_target_blocks();
+    TL_TRY(hipMalloc(&d->xn_d, sizeof(float) * (size_t)(batch < 16 ? batch : 16) * d->dim));
+    TL_TRY(hipMalloc(&d->mpart_d, sizeof(float) * nblk * 2 * 256));
+    TL_TRY(hipMalloc(&d->mcnt_d, sizeof(unsigned) * nblk));
+    TL_TRY(hipMemset(d->mcnt_d, 0, sizeof(unsigned) * nblk));
+  }
   {
     const size_t nsmax = (size_t)((d->S + kAttnChunk - 1) / kAttnChunk);
     const size_t recs = (size_t)batch * d->H * (nsmax > 16 ? nsmax : 16);
@@ -301,6 +309,8 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   (void)hipHostFree(d->pos_h);
   (void)hipFree(d->rope_d);
   (void)hipFree(d->xn_d);
+  (void)hipFree(d->mpart_d);
+  (void)hipFree(d->mcnt_d);
   (void)hipFree(d->part_d);
   (void)hipFree(d->cnt_d);
   (void)hipFree(d->psync);
@@ -337,7 +347,11 @@ extern "C" hipStream_t thallama_decoder_stream(thallama_decoder* d) { return d ?
 // t0..t2 (runq layout) through the int8 kernel (gemv_q8.hpp).
 static hipError_t gemv(thallama_decoder* d, int mode, tl::GemvParams& p, const QuantizedTensor* t0,
                        const QuantizedTensor* t1, const QuantizedTensor* t2) {
-  if (!d->q8) return tl::launch_gemv(mode, p, d->stream, d->nt);
+  if (!d->q8) {
+    p.mpart = d->mpart_d;
+    p.mcnt = d->mcnt_d;
+    return tl::launch_gemv(mode, p, d->stream, d->nt);
+  }
   p.Q0 = t0 ? t0->q : nullptr;
   p.S0 = t0 ? t0->s : nullptr;
   p.Q1 = t1 ? t1->q : nullptr;

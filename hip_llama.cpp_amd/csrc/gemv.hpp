@@ -21,6 +21,7 @@
 //  * Rows are dealt to blocks contiguously and to the 4 waves of a block
 //    interleaved; there is no inter-block communication at all.
 #pragma once
+#include <stdlib.h>
 #include "common.hpp"
 
 namespace tl {
@@ -66,7 +67,24 @@ struct GemvParams {
   // optional scratch [nb][K] for the matrix-core path (gemv_mfma.hpp): when set, the
   // RMSNorm / embedding prologue runs once per launch into it instead of once per block
   float* xn;
+  // optional split-K scratch for the matrix-core path: per-block partial tiles
+  // [tiles][splits][2][256] and one ticket per tile (zero between launches)
+  float* mpart;
+  unsigned* mcnt;
+  int msplit, msteps;    // set by the launcher: K splits per tile, 16-k steps per split
 };
+
+// Blocks the matrix-core GEMV aims for: kMfmaDepth per CU (env THALLAMA_MFMA_DEPTH).
+inline int mfma_target_blocks() {
+  static const int v = [] {
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const char* e = getenv("THALLAMA_MFMA_DEPTH");
+    const int depth = e ? atoi(e) : 4;
+    return ncu * (depth > 0 ? depth : 1);
+  }();
+  return v;
+}
 
 TL_DEVICE float silu_mul(float a, float b) {
   // reference src/seq.cpp:159-166: val *= 1/(1+expf(-val)); val *= hb2

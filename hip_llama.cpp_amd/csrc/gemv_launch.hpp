@@ -17,6 +17,19 @@ inline int gemv_mfma_min_nb() {
   return v;
 }
 
+// Split K across blocks when the row tiles alone leave CUs idle: msplit = target / tiles,
+// at least 2 steps per wave per split; needs the decoder's mpart/mcnt scratch, sized for
+// mfma_target_blocks() tiles x splits.
+inline void mfma_splits(GemvParams& p, int tiles) {
+  const int nsteps = p.K >> 4;
+  int ms = p.mpart && p.mcnt ? mfma_target_blocks() / tiles : 1;
+  const int cap = nsteps / (2 * kMfmaWaves);
+  if (ms > cap) ms = cap;
+  if (ms < 1) ms = 1;
+  p.msteps = (nsteps + ms - 1) / ms;
+  p.msplit = (nsteps + p.msteps - 1) / p.msteps;
+}
+
 template <int MODE, int NB, int IPW, bool NT, int WAVES, bool PF>
 inline void launch_one(const GemvParams& p, hipStream_t s, int kc, size_t lds) {
   const int per_block = WAVES * IPW;
@@ -97,7 +110,9 @@ inline hipError_t launch_mode(const GemvParams& p0, hipStream_t s, const GemvCfg
         p.x_out = nullptr;
       }
       const int rows = MODE == GM_QKV ? 2 * p.n_items : p.n_items;
-      const dim3 grid((rows + 15) / 16);
+      const int tiles = (rows + 15) / 16;
+      mfma_splits(p, tiles);
+      const dim3 grid(tiles * p.msplit);
       if (c.nt) hipLaunchKernelGGL((gemv_mfma_kernel<MODE, true>), grid, dim3(kMfmaWaves * 64), 0, s, p);
       else hipLaunchKernelGGL((gemv_mfma_kernel<MODE, false>), grid, dim3(kMfmaWaves * 64), 0, s, p);
       e = hipGetLastError();

@@ -3,19 +3,19 @@
 // With B sequences the VALU streaming kernel (gemv.hpp) multiplies every weight float4 by B
 // activation float4s read back from LDS: at B = 8 that is 8x the weight bytes in LDS
 // traffic, and the step runs at ~30% of the HBM roofline.  Here one wave computes a 16-row
-// x 16-sequence tile with v_mfma_f32_16x16x4_f32: per 16-k step a lane loads ONE float4 of
-// weights (row l&15, k = 4(l>>4)..+3) and ONE float4 of its sequence's activations
-// (sequence l&15, same k), and four MFMAs consume them (component c of every lane is k-slot
-// l>>4 of MFMA c, so A and B agree on k).  Activations come from L2 (every block reads the
-// same B x K floats); the weights stream once, non-temporal.
+// x 16-sequence tile with v_mfma_f32_16x16x4_f32 (lane (i, q) holds row i / sequence i at
+// k = 4q..4q+3 of each 16-k step; component c feeds MFMA c, so A and B agree on k).
+// Activations come from L2 (every block reads the same B x K floats); the weights stream
+// once, non-temporal.
 //
-// A block is 8 waves on the SAME 16 rows, splitting K (wave w takes 16-k steps w, w+8, ...),
-// so even a 4096-row matrix gives 256 blocks x 8 waves; the 8 partial tiles are summed in
-// LDS in a fixed order (deterministic), then the same fused epilogues as gemv.hpp (store
-// at pos offsets, residual, SwiGLU over a W1/W3 pair of tiles, QKV + RoPE + KV write).
-// Numerics: each wave's partial is a k-ordered fp32 fma chain.  An RMSNorm / embedding
-// prologue runs ONCE per launch (gemv_prenorm_kernel, x' = w * (ss * x) as in
-// src/seq.cpp:3-16) into scratch rows, not once per block.
+// The launcher splits K across blocks until the grid fills every CU four blocks deep (a
+// 4096-row matrix -> 256 tiles x 4 splits).  Wave partials are summed in LDS and split
+// partials by the last block of the tile, both in a fixed order (deterministic), then the
+// same fused epilogues as gemv.hpp (store at pos offsets, residual, SwiGLU over a W1/W3
+// pair of tiles, QKV + RoPE + KV write).  An RMSNorm / embedding prologue runs ONCE per
+// launch (gemv_prenorm_kernel, x' = w * (ss * x) as in src/seq.cpp:3-16) into scratch
+// rows, not once per block.  The fp32 MFMA accumulates exactly-rounded products in fp32,
+// within the reference's 1e-4 logits tolerance of its sequential loop.
 #pragma once
 #include "gemv.hpp"
 
@@ -23,8 +23,7 @@ namespace tl {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kMfmaWaves = 8;
-constexpr int kMfmaUnr = 8;
+constexpr int kMfmaWaves = 4;
 
 // One output of the decode epilogues (gemv.hpp epilogue) for row/item `item`, sequence b.
 template <int MODE>
@@ -92,118 +91,171 @@ static __global__ void __launch_bounds__(256) gemv_prenorm_kernel(GemvParams p) 
   }
 }
 
+// Block = kMfmaWaves waves on one 16-row tile and one K split (blockIdx = tile * msplit +
+// split); wave w takes a contiguous run of the split's 16-k steps.  Per group of U 16-k steps a wave reads its
+// 16-row weight tile (and the 16 activation rows) as 256-B contiguous runs per row (16
+// lanes x 16 B, four rows per instruction), writes them to a wave-private LDS tile (rows
+// padded by 16 B: conflict-free both ways) and reads them back in the MFMA lane layout
+// (lane (i, q): row i, k = 16 u + 4 q).  Loading the MFMA layout straight from HBM (64 B
+// per row per instruction) ran at 2.5-3.5 TB/s, these runs at 3.5-5.4 TB/s (profiles/
+// r01_mfma_sweep.jsonl); LDS traffic is ~1 B per weight byte.  The weights of group g + 1
+// are in flight while group g multiplies; steps past the run load a clamped (valid)
+// address and multiply zero activations, so no load is predicated.
 template <int MODE, bool NT>
 __global__ void __launch_bounds__(kMfmaWaves * 64) gemv_mfma_kernel(GemvParams p) {
-  constexpr int W = kMfmaWaves, U = kMfmaUnr;
-  constexpr bool TWO = MODE == GM_SWIGLU;  // two weight tiles (W1, W3) share the activations
-  __shared__ float red[W][TWO ? 2 : 1][256];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int W = kMfmaWaves;
+  constexpr bool TWO = MODE == GM_SWIGLU;
+  constexpr int NR = TWO ? 2 : 1;      // weight tiles per group; tile NR is the activations
+  constexpr int U = 4;                 // 16-k steps per group
+  constexpr int LPR = U * 4;           // lanes per row in a load (16 B each): 256-B runs
+  constexpr int RPI = 64 / LPR;        // rows per load instruction
+  constexpr int NI = 16 / RPI;         // load instructions per 16-row tile
+  constexpr int STR = U * 16 + 4;      // LDS row stride in floats (padded)
+  constexpr int TILE = 16 * STR;       // floats per tile
+  __shared__ __attribute__((aligned(16))) float lds[W * (NR + 1) * TILE];
+  __shared__ unsigned s_last;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int i = lane & 15, q = lane >> 4;
+  const int lr = lane / LPR, lc = lane % LPR;  // load map: row RPI v + lr, 16-B chunk lc
   const int K = p.K, nb = p.nb;
   const long long Kl = K;
-
-  // this lane's weight row(s): tile of 16 rows (QKV: 8 row pairs; SwiGLU: 16 items)
+  const int tile = blockIdx.x / p.msplit, split = blockIdx.x - tile * p.msplit;
   const int n_rows = MODE == GM_QKV ? 2 * p.n_items : p.n_items;
-  const int r = blockIdx.x * 16 + i;
-  const bool rv = r < n_rows;
-  const int rr = rv ? r : 0;
-  const float* w0;
-  const float* w1 = nullptr;
-  if constexpr (MODE == GM_SWIGLU) {
-    w0 = p.W0 + rr * Kl;
-    w1 = p.W1 + rr * Kl;
-  } else if constexpr (MODE == GM_QKV) {
-    w0 = item_row<GM_QKV>(p, rr >> 1, rr & 1);
-  } else {
-    w0 = p.W0 + rr * Kl;
+
+  const float* wrow[NR][NI];
+  const float* xrow[NI];
+  bool xok[NI];
+#pragma unroll
+  for (int v = 0; v < NI; ++v) {
+    const int r = RPI * v + lr;
+    int R = tile * 16 + r;
+    R = R < n_rows ? R : n_rows - 1;
+    if constexpr (MODE == GM_SWIGLU) {
+      wrow[0][v] = p.W0 + R * Kl;
+      wrow[NR - 1][v] = p.W1 + R * Kl;
+    } else if constexpr (MODE == GM_QKV) {
+      wrow[0][v] = item_row<GM_QKV>(p, R >> 1, R & 1);
+    } else {
+      wrow[0][v] = p.W0 + R * Kl;
+    }
+    xok[v] = r < nb;
+    xrow[v] = p.x + (long long)(r < nb ? r : 0) * p.x_stride;
   }
-  // this lane's sequence (column i); the launcher has already applied any RMSNorm /
-  // embedding prologue (gemv_prenorm_kernel), so x holds the GEMV input rows
-  const bool jv = i < nb;
-  const float* xr = jv ? p.x + (long long)i * p.x_stride : nullptr;
 
   const int nsteps = K >> 4;
-  auto wl = [&](const float* w, int s) {
-    const f4* a = reinterpret_cast<const f4*>(w + 16 * s + 4 * q);
+  const int s0 = split * p.msteps;
+  const int s1 = s0 + p.msteps < nsteps ? s0 + p.msteps : nsteps;
+  const int per = (s1 - s0 + W * U - 1) / (W * U) * U;
+  const int ws = s0 + wave * per;
+  const int we = ws + per < s1 ? ws + per : s1;
+  const int ng = we > ws ? (we - ws + U - 1) / U : 0;
+  // this lane's float offset in group g (clamped to a valid address past the run)
+  auto kof = [&](int g, bool& ok) {
+    const int st = ws + g * U + (lc >> 2);
+    ok = st < we;
+    return ok ? 16 * (ws + g * U) + 4 * lc : 16 * (nsteps - 1) + 4 * (lc & 3);
+  };
+  auto wl = [&](const float* w) {
+    const f4* a = reinterpret_cast<const f4*>(w);
     if constexpr (NT) return __builtin_nontemporal_load(a);
     else return *a;
   };
-
-  f4 wa[U], wb[U];
+  auto load = [&](f4 (&t)[NR + 1][NI], int g) {
+    bool ok;
+    const int k = kof(g, ok);
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int s = wave + W * u;
-    if (s < nsteps) {
-      wa[u] = wl(w0, s);
-      if constexpr (TWO) wb[u] = wl(w1, s);
+    for (int v = 0; v < NI; ++v) {
+#pragma unroll
+      for (int m = 0; m < NR; ++m) t[m][v] = wl(wrow[m][v] + k);
+      const f4 x = *reinterpret_cast<const f4*>(xrow[v] + k);
+      t[NR][v] = (ok && xok[v]) ? x : f4{0.f, 0.f, 0.f, 0.f};
     }
-  }
-
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  for (int g = 0; g * W * U < nsteps; ++g) {
-    f4 xv[U];
+  };
+  float* my = lds + wave * (NR + 1) * TILE;
+  f32x4 acc[NR];
+#pragma unroll
+  for (int m = 0; m < NR; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const f4 (&t)[NR + 1][NI]) {
+#pragma unroll
+    for (int m = 0; m <= NR; ++m)
+#pragma unroll
+      for (int v = 0; v < NI; ++v)
+        *reinterpret_cast<f4*>(my + m * TILE + (RPI * v + lr) * STR + 4 * lc) = t[m][v];
+    asm volatile("" ::: "memory");  // same-wave LDS ops execute in order
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int s = wave + W * (g * U + u);
-      xv[u] = f4{0.f, 0.f, 0.f, 0.f};
-      if (s < nsteps && jv) xv[u] = *reinterpret_cast<const f4*>(xr + 16 * s + 4 * q);
-    }
+      const f4 x = *reinterpret_cast<const f4*>(my + NR * TILE + i * STR + 16 * u + 4 * q);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int s = wave + W * (g * U + u);
-      if (s < nsteps) {
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[u].x, xv[u].x, acc0, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[u].y, xv[u].y, acc0, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[u].z, xv[u].z, acc0, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[u].w, xv[u].w, acc0, 0, 0, 0);
-        if constexpr (TWO) {
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[u].x, xv[u].x, acc1, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[u].y, xv[u].y, acc1, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[u].z, xv[u].z, acc1, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[u].w, xv[u].w, acc1, 0, 0, 0);
-        }
+      for (int m = 0; m < NR; ++m) {
+        const f4 a = *reinterpret_cast<const f4*>(my + m * TILE + i * STR + 16 * u + 4 * q);
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, x.x, acc[m], 0, 0, 0);
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, x.y, acc[m], 0, 0, 0);
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, x.z, acc[m], 0, 0, 0);
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, x.w, acc[m], 0, 0, 0);
       }
     }
-    // next group's weights
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int s = wave + W * ((g + 1) * U + u);
-      if (s < nsteps) {
-        wa[u] = wl(w0, s);
-        if constexpr (TWO) wb[u] = wl(w1, s);
-      }
-    }
+    asm volatile("" ::: "memory");
+  };
+
+  f4 ta[NR + 1][NI], tb[NR + 1][NI];
+  if (ng > 0) load(ta, 0);
+  for (int g = 0; g < ng; g += 2) {
+    if (g + 1 < ng) load(tb, g + 1);
+    mma(ta);
+    if (g + 1 >= ng) break;
+    if (g + 2 < ng) load(ta, g + 2);
+    mma(tb);
   }
 
-  // C layout (16x16): lane holds rows 4q..4q+3 of column i
+  __syncthreads();  // the staging tiles become the wave-partial buffer
+  float* red = lds;  // [W][NR][256]
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    red[wave][0][(4 * q + e) * 16 + i] = acc0[e];
-    if constexpr (TWO) red[wave][TWO ? 1 : 0][(4 * q + e) * 16 + i] = acc1[e];
-  }
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int m = 0; m < NR; ++m) red[(wave * NR + m) * 256 + (4 * q + e) * 16 + i] = acc[m][e];
   __syncthreads();
-  const int t = threadIdx.x;
-  if (t < 256) {
+  auto wsum = [&](int m, int t) {
+    float v = red[m * 256 + t];
+    for (int w = 1; w < W; ++w) v += red[(w * NR + m) * 256 + t];
+    return v;
+  };
+  const int msplit = p.msplit;
+  float* tpart = p.mpart + (long long)tile * msplit * (NR * 256);
+  if (msplit > 1) {
+    for (int t = threadIdx.x; t < 256; t += W * 64) {
+      st1_sc1(tpart + split * (NR * 256) + t, wsum(0, t));
+      if constexpr (TWO) st1_sc1(tpart + split * (NR * 256) + 256 + t, wsum(1, t));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      s_last = __hip_atomic_fetch_add(p.mcnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               (unsigned)(msplit - 1);
+    __syncthreads();
+    if (!s_last) return;
+  }
+  auto tot = [&](int m, int t) {
+    if (msplit == 1) return wsum(m, t);
+    const float* b = tpart + m * 256 + t;
+    float v = ld1_sc1(b);
+    for (int sp = 1; sp < msplit; ++sp) v += ld1_sc1(b + sp * (NR * 256));
+    return v;
+  };
+  for (int t = threadIdx.x; t < 256; t += W * 64) {
     const int row = t >> 4, j = t & 15;
-    const int R = blockIdx.x * 16 + row;
+    const int R = tile * 16 + row;
     if (j < nb && R < n_rows) {
-      float v0 = red[0][0][t];
-      for (int w = 1; w < W; ++w) v0 += red[w][0][t];
       if constexpr (MODE == GM_SWIGLU) {
-        float v1 = red[0][TWO ? 1 : 0][t];
-        for (int w = 1; w < W; ++w) v1 += red[w][TWO ? 1 : 0][t];
-        epi_one<MODE>(p, R, j, v0, v1);
+        epi_one<MODE>(p, R, j, tot(0, t), tot(NR - 1, t));
       } else if constexpr (MODE == GM_QKV) {
-        if ((row & 1) == 0) {
-          float v1 = red[0][0][t + 16];
-          for (int w = 1; w < W; ++w) v1 += red[w][0][t + 16];
-          epi_one<MODE>(p, R >> 1, j, v0, v1);
-        }
+        if ((row & 1) == 0) epi_one<MODE>(p, R >> 1, j, tot(0, t), tot(0, t + 16));
       } else {
-        epi_one<MODE>(p, R, j, v0, 0.f);
+        epi_one<MODE>(p, R, j, tot(0, t), 0.f);
       }
     }
   }
+  if (msplit > 1 && threadIdx.x == 0) __hip_atomic_store(p.mcnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace tl
