@@ -219,6 +219,22 @@ static int replica_step(void* ctx, int worker, int batch, const int* token, cons
   return st;
 }
 
+// batched prompt processing (thallama_decoder_prefill); > 0 = not supported here (int8, or
+// THALLAMA_NO_PREFILL=1), so the scheduler steps through the prompt like the reference
+static int prefill_on(Replica& r, int slot, const int* tokens, int n, int pos0) {
+  static const bool off = getenv("THALLAMA_NO_PREFILL") && atoi(getenv("THALLAMA_NO_PREFILL")) != 0;
+  if (off) return 1;
+  if (hipSetDevice(r.dev) != hipSuccess) return -3;
+  const int st = thallama_decoder_prefill(r.dec, slot, tokens, n, pos0);
+  if (st == (int)hipErrorNotSupported) return 1;
+  if (st) fprintf(stderr, "device %d prefill: %s\n", r.dev, thallama_last_error());
+  return st ? -st : 0;
+}
+
+static int replica_prefill(void* ctx, int worker, int slot, const int* tokens, int n, int pos0) {
+  return prefill_on((*(std::vector<Replica>*)ctx)[worker], slot, tokens, n, pos0);
+}
+
 // generate mode (src/llama.cpp:522-579), on GPU 0
 static void generate(const Config& cfg, Replica& r, thallama_tokenizer* tok, thallama_sampler* smp, const char* prompt,
                      int steps) {
@@ -233,6 +249,20 @@ static void generate(const Config& cfg, Replica& r, thallama_tokenizer* tok, tha
   std::vector<float> logits((size_t)cfg.vocab_size);
   long start = 0;
   int token = ids[0], pos = 0;
+  // prompt tokens 0..m-1 in one prefill instead of m forced decode steps (same pieces)
+  int m = n_ids - 1 < steps ? n_ids - 1 : steps;
+  for (int i = 1; i <= m && i < n_ids; ++i)
+    if (ids[i] == 1) m = 0;  // the prompt would end the loop: step through it instead
+  if (m >= 1 && prefill_on(r, 0, ids.data(), m, 0) == 0) {
+    for (int i = 0; i < m; ++i) {
+      const char* piece = thallama_tokenizer_decode(tok, ids[i], ids[i + 1]);
+      if (thallama_piece_is_safe(piece)) printf("%s", piece);
+    }
+    fflush(stdout);
+    token = ids[m];
+    pos = m;
+    start = time_in_ms();
+  }
   while (pos < steps) {
     if (thallama_decoder_forward(r.dec, &token, &pos, logits.data()) != 0) {
       fprintf(stderr, "forward: %s\n", thallama_last_error());
@@ -333,7 +363,8 @@ int main(int argc, char* argv[]) {
 
     const long start = time_in_ms();
     long long num_gen_tokens = 0;
-    const int st = thallama_serve_requests(req, tokenizer_path, V, n_dev, batch, replica_step, &reps, &num_gen_tokens);
+    const int st = thallama_serve_requests_prefill(req, tokenizer_path, V, n_dev, batch, replica_step, replica_prefill,
+                                                   &reps, &num_gen_tokens);
     const long end = time_in_ms();
     if (st != 0) {
       fprintf(stderr, "test mode failed (%d)\n", st);

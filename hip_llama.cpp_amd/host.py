@@ -10,6 +10,7 @@ _LIB = None
 HERE = os.path.dirname(os.path.abspath(__file__))
 STEP_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
                       C.POINTER(C.c_float))
+PREFILL_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int), C.c_int, C.c_int)
 
 
 def lib():
@@ -47,6 +48,8 @@ def lib():
             "thallama_requests_output": (S, [VP, I]),
             "thallama_requests_write": (I, [VP, S]),
             "thallama_serve_requests": (I, [VP, S, I, I, I, STEP_FN, VP, C.POINTER(C.c_longlong)]),
+            "thallama_serve_requests_prefill": (I, [VP, S, I, I, I, STEP_FN, PREFILL_FN, VP,
+                                                    C.POINTER(C.c_longlong)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -130,8 +133,9 @@ class Requests:
         if lib().thallama_requests_write(self.h, path.encode()):
             raise RuntimeError(f"cannot write {path}")
 
-    def serve(self, tokenizer_path, vocab_size, n_workers, batch, step):
-        """step(worker, tokens[batch], pos[batch]) -> logits [batch, vocab] float32."""
+    def serve(self, tokenizer_path, vocab_size, n_workers, batch, step, prefill=None):
+        """step(worker, tokens[batch], pos[batch]) -> logits [batch, vocab] float32;
+        prefill(worker, slot, tokens[n], pos0) -> 0 (done) / 1 (not supported), optional."""
         def cb(_ctx, worker, b, tok, pos, out):
             try:
                 lg = step(worker, np.ctypeslib.as_array(tok, (b,)).copy(), np.ctypeslib.as_array(pos, (b,)).copy())
@@ -141,10 +145,23 @@ class Requests:
                 import traceback
                 traceback.print_exc()
                 return 7
+
+        def pcb(_ctx, worker, slot, tok, n, pos0):
+            try:
+                return int(prefill(worker, slot, np.ctypeslib.as_array(tok, (n,)).copy(), pos0))
+            except Exception:  # noqa: BLE001
+                import traceback
+                traceback.print_exc()
+                return -7
         fn = STEP_FN(cb)
         gen = C.c_longlong(0)
-        st = lib().thallama_serve_requests(self.h, tokenizer_path.encode(), vocab_size, n_workers, batch, fn, None,
-                                          C.byref(gen))
+        if prefill is None:
+            st = lib().thallama_serve_requests(self.h, tokenizer_path.encode(), vocab_size, n_workers, batch, fn,
+                                              None, C.byref(gen))
+        else:
+            pfn = PREFILL_FN(pcb)
+            st = lib().thallama_serve_requests_prefill(self.h, tokenizer_path.encode(), vocab_size, n_workers,
+                                                      batch, fn, pfn, None, C.byref(gen))
         if st:
             raise RuntimeError(f"serve_requests failed: {st}")
         return gen.value

@@ -294,6 +294,13 @@ extern "C" int thallama_requests_write(const thallama_requests* r, const char* p
 extern "C" int thallama_serve_requests(thallama_requests* r, const char* tokenizer_path, int vocab_size,
                                        int n_workers, int batch, thallama_step_fn step, void* ctx,
                                        long long* gen_tokens) {
+  return thallama_serve_requests_prefill(r, tokenizer_path, vocab_size, n_workers, batch, step, nullptr, ctx,
+                                         gen_tokens);
+}
+
+extern "C" int thallama_serve_requests_prefill(thallama_requests* r, const char* tokenizer_path, int vocab_size,
+                                               int n_workers, int batch, thallama_step_fn step,
+                                               thallama_prefill_fn prefill, void* ctx, long long* gen_tokens) {
   if (!r || !step || n_workers <= 0 || batch <= 0) return -1;
   const int n_req = (int)r->prompts.size();
   const int V = vocab_size;
@@ -339,7 +346,31 @@ extern "C" int thallama_serve_requests(thallama_requests* r, const char* tokeniz
         pos[b] = 0;
         steps[b] = r->max_seq_len;
         done[b] = 0;
+        // Batched prompt: the reference feeds prompt tokens 0..n-2 one decode step each,
+        // ignoring their logits (src/llama.cpp:1029-1031).  Processing them in one prefill
+        // leaves the slot exactly where those steps would: pos = n-1, token = prompt[n-1],
+        // the prompt pieces in the text.  Skipped when the prompt itself would end the
+        // sequence (a BOS/EOS id past position 0, or longer than max_seq_len).
+        const int m = n_prompt[b] - 1;
+        bool ok = prefill && m >= 1 && m < steps[b];
+        for (int i = 1; ok && i <= m; ++i) ok = prompt[b][i] != 1 && prompt[b][i] != 2;
+        if (ok) {
+          const int pst = prefill(ctx, w, b, prompt[b].data(), m, 0);
+          if (pst < 0) {
+            status = pst;
+            break;
+          }
+          if (pst == 0) {
+            for (int i = 0; i < m; ++i) {
+              const char* piece = thallama_tokenizer_decode(tok, prompt[b][i], prompt[b][i + 1]);
+              if (thallama_piece_is_safe(piece)) text[b] += piece;
+            }
+            token[b] = prompt[b][m];
+            pos[b] = m;
+          }
+        }
       }
+      if (status != 0) break;
       if (idle == batch) break;
       const int st = step(ctx, w, batch, token.data(), pos.data(), logits.data());
       if (st != 0) {

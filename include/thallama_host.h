@@ -68,6 +68,16 @@ typedef int (*thallama_step_fn)(void* ctx, int worker, int batch, const int* tok
  * *gen_tokens = the reference's num_gen_tokens.  Returns 0, or the first nonzero step status. */
 int thallama_serve_requests(thallama_requests* r, const char* tokenizer_path, int vocab_size, int n_workers,
                             int batch, thallama_step_fn step, void* ctx, long long* gen_tokens);
+/* Prompt processing for slot `slot` of worker `worker`: tokens[0..n) at positions pos0.. into
+ * that slot's KV cache, logits not needed.  Returns 0 when done, > 0 when the replica cannot
+ * (the scheduler then steps through the prompt), < 0 on error. */
+typedef int (*thallama_prefill_fn)(void* ctx, int worker, int slot, const int* tokens, int n, int pos0);
+/* thallama_serve_requests with batched prompts: a newly admitted request's prompt tokens
+ * 0..n-2 go through `prefill` (when non-null) instead of n-1 decode steps; the outputs and
+ * *gen_tokens are those of thallama_serve_requests (identical up to the logits tolerance). */
+int thallama_serve_requests_prefill(thallama_requests* r, const char* tokenizer_path, int vocab_size,
+                                    int n_workers, int batch, thallama_step_fn step, thallama_prefill_fn prefill,
+                                    void* ctx, long long* gen_tokens);
 
 #ifdef __cplusplus
 }

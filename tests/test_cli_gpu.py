@@ -23,7 +23,7 @@ TOK = os.path.join(REPO, "tests", "golden", "tokenizer.bin")
 CFG = (256, 768, 2, 4, 4, 32000, 96)   # head 64; unshared classifier
 V = 32000
 PROMPTS = ["Once upon a time", "The serene landscape of the countryside was", "", "A brief message:",
-           "héllo wörld", "Why is the sky blue?"]
+           "héllo wörld", "Why is the sky blue?", "The serene landscape of the countryside was calm. " * 4]
 
 
 @pytest.fixture(scope="module")
@@ -66,20 +66,25 @@ def expected_test_mode(host, ref, prompts, seq_len):
     return outs, gen
 
 
-def run_cli(args, cwd):
+def run_cli(args, cwd, env=None):
     assert os.path.exists(RUN), "build the CLI: make -C hip_llama.cpp_amd"
-    r = subprocess.run([RUN] + args, cwd=cwd, capture_output=True, timeout=300)
+    r = subprocess.run([RUN] + args, cwd=cwd, capture_output=True, timeout=300,
+                       env=None if env is None else {**os.environ, **env})
     assert r.returncode == 0, r.stderr.decode()[-2000:]
     return r
 
 
+@pytest.mark.parametrize("prefill", [True, False])
 @pytest.mark.parametrize("batch", [1, 3])
-def test_test_mode_output_file_byte_identical(gpu, host, model, tmp_path, batch):
+def test_test_mode_output_file_byte_identical(gpu, host, model, tmp_path, batch, prefill):
+    """Prompts go through the batched prefill by default (THALLAMA_NO_PREFILL=1 steps through
+    them like the reference); the output file is the same either way."""
     ref, path = model
     inp = tmp_path / "in.txt"
     inp.write_bytes((f"{len(PROMPTS)}\n" + "\n".join(PROMPTS) + "\n").encode())
     out = tmp_path / "out.txt"
-    r = run_cli([path, "-m", "test", "-f", str(inp), "-o", str(out), "-b", str(batch), "-z", TOK], tmp_path)
+    r = run_cli([path, "-m", "test", "-f", str(inp), "-o", str(out), "-b", str(batch), "-z", TOK], tmp_path,
+                env={"THALLAMA_NO_PREFILL": "0" if prefill else "1"})
     want, gen = expected_test_mode(host, ref, PROMPTS, CFG[6])
     assert out.read_bytes() == f"{len(PROMPTS)}\n".encode() + b"".join(w + b"\n" for w in want)
     assert f"Total achieved token: {gen}".encode() in r.stdout

@@ -214,3 +214,83 @@ def test_scheduler_outputs_independent_of_placement(host, tok, tmp_path, workers
     out = tmp_path / "out.txt"
     r.write(str(out))
     assert out.read_bytes() == f"{len(prompts)}\n".encode() + b"".join(w + b"\n" for w in want)
+
+
+class _ChainModel:
+    """A stateful stand-in for the decoder: each slot carries a hash of every (token, pos) it
+    has processed since position 0, and the logits are drawn from that hash.  A prefill that
+    skipped, reordered or misplaced a prompt token would change every later distribution."""
+
+    def __init__(self):
+        self.h = {}
+
+    @staticmethod
+    def mix(h, token, pos):
+        return (h * 1000003 + int(token) * 7919 + int(pos) * 104729 + 1) % (1 << 61)
+
+    def feed(self, key, token, pos):
+        h = 17 if pos == 0 else self.h[key]
+        self.h[key] = self.mix(h, token, pos)
+        return self.h[key]
+
+    @staticmethod
+    def logits(h, pos):
+        r = np.random.default_rng(h)
+        lg = (r.standard_normal(V) * 2.5).astype(np.float32)
+        lg[2] = np.float32(-4.0 + 0.25 * pos)
+        return lg
+
+
+@pytest.mark.parametrize("workers,batch,support", [(1, 1, 0), (1, 3, 0), (2, 2, 0), (3, 5, 0), (2, 3, 1)])
+def test_scheduler_prefill_matches_stepping(host, tok, tmp_path, workers, batch, support):
+    """thallama_serve_requests_prefill: prompts through a prefill callback give the outputs and
+    generated-token count of the stepping scheduler (src/llama.cpp:1029-1031); a callback that
+    declines (returns 1) falls back to stepping."""
+    src = tmp_path / "in.txt"
+    prompts = ["Once upon a time there was", "The serene landscape", "", "héllo wörld", "x" * 60, "Why?",
+               "A brief message: " * 3]
+    src.write_bytes((f"{len(prompts)}\n" + "\n".join(prompts) + "\n").encode())
+    seq_len = 40
+
+    def expected():
+        m = _ChainModel()
+        outs, gen = [], 0
+        for i, p in enumerate(prompts):
+            ids = tok.encode(p.encode())
+            smp = host.Sampler(V, 1.0, 0.9, 314028)
+            token, pos, text = ids[0], 0, b""
+            while True:
+                lg = m.logits(m.feed(i, token, pos), pos)
+                nxt = ids[pos + 1] if pos < len(ids) - 1 else smp.sample(lg)
+                pos += 1
+                if nxt in (1, 2):
+                    break
+                if tok.is_safe(token, nxt):
+                    text += tok.decode(token, nxt)
+                token = nxt
+                if pos >= seq_len:
+                    break
+            outs.append(text + b"\n")
+            gen += pos - 1
+        return outs, gen
+
+    model, calls = _ChainModel(), []
+
+    def step(worker, toks, pos):
+        return np.stack([model.logits(model.feed((worker, b), t, p), p) for b, (t, p) in enumerate(zip(toks, pos))])
+
+    def prefill(worker, slot, toks, pos0):
+        calls.append(len(toks))
+        if support:
+            return 1
+        for i, t in enumerate(toks):
+            model.feed((worker, slot), t, pos0 + i)
+        return 0
+    r = host.Requests(str(src), 27, seq_len)
+    gen = r.serve(TOK, V, workers, batch, step, prefill)
+    want, want_gen = expected()
+    assert [r.output(i) for i in range(len(prompts))] == want
+    assert gen == want_gen
+    # every prompt of >= 2 tokens that fits seq_len went through the callback once
+    lens = [len(tok.encode(p.encode())) for p in prompts]
+    assert sorted(calls) == sorted(n - 1 for n in lens if 2 <= n and n - 1 < seq_len)
