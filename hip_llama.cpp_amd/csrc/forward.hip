@@ -142,6 +142,7 @@ struct thallama_decoder {
   size_t psync_zero = 0;        // words zeroed before every launch
   unsigned long long* pbmax = nullptr;
   unsigned long long* pgran = nullptr;  // hand-off granules: x | xb | hb | qkv
+  unsigned long long* pq8tab = nullptr; // int8: per-layer (int8, scale) addresses [7][L][2]
   bool pok = false;             // shape supported
   unsigned long long* ptrace = nullptr;  // optional timeline of the persistent step
   size_t ptrace_n = 0;
@@ -316,6 +317,7 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   (void)hipFree(d->psync);
   (void)hipFree(d->pbmax);
   (void)hipFree(d->pgran);
+  (void)hipFree(d->pq8tab);
   (void)hipFree(d->ptrace);
   for (void* b : {(void*)d->pf_x, (void*)d->pf_xn, (void*)d->pf_q, (void*)d->pf_xb, (void*)d->pf_hb,
                   (void*)d->pf_part, (void*)d->pf_cnt, (void*)d->pf_tok, (void*)d->pf_pos})
@@ -538,7 +540,7 @@ static int enqueue_step(thallama_decoder* d) {
   return 0;
 }
 
-static bool use_persist(const thallama_decoder* d) { return d->persist && d->pok && !d->q8; }
+static bool use_persist(const thallama_decoder* d) { return d->persist && d->pok; }
 
 // The whole step (and, for greedy decoding, the argmax + advance) as one persistent launch.
 static int enqueue_persistent(thallama_decoder* d, bool argmax) {
@@ -558,6 +560,12 @@ static int enqueue_persistent(thallama_decoder* d, bool argmax) {
   p.err = d->psync + d->psync_zero; p.seq = p.err + 1; p.bmax = d->pbmax;
   p.argmax = argmax ? 1 : 0;
   p.trace = d->ptrace;
+  if (d->q8) {
+    p.q8 = d->w8.group_size;
+    p.q8tab = d->pq8tab;
+    p.qcls = d->w8.wcls->q;
+    p.scls = d->w8.wcls->s;
+  }
   const char* why = nullptr;
   if (!tl::persistent_prepare(p, d->ncu, &why)) {
     g_last_error = std::string("persistent step: ") + (why ? why : "unsupported");
@@ -812,8 +820,30 @@ extern "C" int thallama_decoder_create_q8(thallama_decoder** out, const Config* 
   w.rms_final_weight = w8->rms_final_weight;
   const int r = thallama_decoder_create(out, cfg, &w, s, batch, stream);
   if (r) return r;
-  (*out)->q8 = true;
-  (*out)->w8 = *w8;
+  thallama_decoder* d = *out;
+  d->q8 = true;
+  d->w8 = *w8;
+  // persistent step with int8 weights: re-check the shape (group size, LDS) and publish the
+  // per-layer tensor addresses as a device table the kernel indexes by (tensor, layer)
+  if (d->pok) {
+    tl::PStep ps = {};
+    ps.dim = d->dim; ps.hid = d->hidden; ps.kvd = d->kv_dim; ps.hs = d->hs; ps.NS = d->nsplit; ps.L = d->L;
+    ps.q8 = w8->group_size;
+    const char* why = nullptr;
+    d->pok = tl::persistent_prepare(ps, d->ncu, &why);
+    if (!d->pok && why) d->pwhy = why;
+  }
+  if (d->pok) {
+    const QuantizedTensor* ts[7] = {w8->wq, w8->wk, w8->wv, w8->wo, w8->w1, w8->w2, w8->w3};
+    std::vector<unsigned long long> tab((size_t)7 * d->L * 2);
+    for (int t = 0; t < 7; ++t)
+      for (int l = 0; l < d->L; ++l) {
+        tab[((size_t)t * d->L + l) * 2] = (unsigned long long)(uintptr_t)ts[t][l].q;
+        tab[((size_t)t * d->L + l) * 2 + 1] = (unsigned long long)(uintptr_t)ts[t][l].s;
+      }
+    TL_TRY(hipMalloc(&d->pq8tab, sizeof(unsigned long long) * (tab.size() > 0 ? tab.size() : 1)));
+    TL_TRY(hipMemcpy(d->pq8tab, tab.data(), sizeof(unsigned long long) * tab.size(), hipMemcpyHostToDevice));
+  }
   return 0;
 }
 

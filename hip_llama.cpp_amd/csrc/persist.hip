@@ -1,4 +1,4 @@
-// persist.hip — the whole batch-1 fp32 decode step as ONE persistent launch.
+// persist.hip — the whole batch-1 decode step as ONE persistent launch (fp32 or Q8_0 weights).
 //
 // Semantics: the reference forward (src/seq.cpp:53-168; GPU twin src/thaDNN.cpp:13-260)
 // followed, in greedy mode, by sample_argmax (src/llama.cpp:275-286).
@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 #include "attention.hpp"
 #include "gemv.hpp"
+#include "gemv_q8.hpp"
 #include "persist.hpp"
 
 namespace tl {
@@ -57,6 +58,7 @@ struct PDesc {
   const float* W0;               // QKV: Wq | W1 (SwiGLU) | W
   const float* W1;               // QKV: Wk | W3
   const float* W2;               // QKV: Wv
+  const float *S0, *S1, *S2;     // Q8: the matching scale blocks (W* then point at int8 rows)
   const unsigned long long* gin; // input granules (null: the token's embedding row)
   unsigned tag_in;
   const float* rms;              // fused RMSNorm weight or null
@@ -64,6 +66,7 @@ struct PDesc {
   unsigned tag_out;
 };
 
+template <bool Q8>
 TL_DEVICE PDesc make_desc(const PStep& p, int kind, int l, unsigned tb) {
   PDesc d = {};
   d.kind = kind;
@@ -94,35 +97,52 @@ TL_DEVICE PDesc make_desc(const PStep& p, int kind, int l, unsigned tb) {
       d.W0 = p.wcls; d.gin = p.L == 0 ? nullptr : p.gx; d.tag_in = tb + 5u * p.L; d.rms = p.rms_final;
       break;
   }
+  if constexpr (Q8) {
+    // per-layer (int8, scale) pairs: table [tensor][L][2], tensors wq wk wv wo w1 w2 w3
+    auto q = [&](int t, int i) { return reinterpret_cast<const float*>(p.q8tab[((long long)t * p.L + l) * 2 + i]); };
+    switch (kind) {
+      case PK_QKV: d.W0 = q(0, 0); d.S0 = q(0, 1); d.W1 = q(1, 0); d.S1 = q(1, 1); d.W2 = q(2, 0); d.S2 = q(2, 1); break;
+      case PK_WO: d.W0 = q(3, 0); d.S0 = q(3, 1); break;
+      case PK_UP: d.W0 = q(4, 0); d.S0 = q(4, 1); d.W1 = q(6, 0); d.S1 = q(6, 1); break;
+      case PK_DOWN: d.W0 = q(5, 0); d.S0 = q(5, 1); break;
+      default: d.W0 = reinterpret_cast<const float*>(p.qcls); d.S0 = p.scls; break;
+    }
+  }
   return d;
 }
 
 // The GEMV phase that follows `kind` at layer l (attention has no weights).
+template <bool Q8>
 TL_DEVICE PDesc next_desc(const PStep& p, int kind, int l, unsigned tb) {
-  if (kind == PK_QKV) return make_desc(p, PK_WO, l, tb);
-  if (kind == PK_WO) return make_desc(p, PK_UP, l, tb);
-  if (kind == PK_UP) return make_desc(p, PK_DOWN, l, tb);
-  return l + 1 < p.L ? make_desc(p, PK_QKV, l + 1, tb) : make_desc(p, PK_CLS, p.L, tb);
+  if (kind == PK_QKV) return make_desc<Q8>(p, PK_WO, l, tb);
+  if (kind == PK_WO) return make_desc<Q8>(p, PK_UP, l, tb);
+  if (kind == PK_UP) return make_desc<Q8>(p, PK_DOWN, l, tb);
+  return l + 1 < p.L ? make_desc<Q8>(p, PK_QKV, l + 1, tb) : make_desc<Q8>(p, PK_CLS, p.L, tb);
 }
 
-// Geometry of a phase for this block (all wave-uniform).  A slot is one 8-KiB chunk of one
-// row: row rl of the block, floats [c*2048, c*2048 + 2048).
+// Geometry of a phase for this block (all wave-uniform).  fp32: a slot is one 8-KiB chunk
+// of one row (row rl of the block, floats [c*2048, c*2048 + 2048)) and has one result.
+// Q8: a chunk is 4 KiB of one int8 row (one result each) and a slot is two consecutive
+// chunks, which may belong to two rows (a 4096-wide int8 row is one chunk).
 struct PGeo {
   int rowb;  // row length in bytes
-  int nch;   // chunks per row
+  int nch;   // chunks (results) per row
   int i0;    // first item of this block
   int ni;    // items of this block
-  int nslot; // slots of this block (ni * rpi * nch)
+  int nres;  // results of this block (ni * rpi * nch)
+  int nslot; // slots of this block
 };
 
+template <bool Q8>
 TL_DEVICE PGeo geo(const PDesc& d) {
   PGeo g;
-  g.rowb = d.K * 4;
-  g.nch = (d.K + PL * 256 - 1) / (PL * 256);
+  g.rowb = Q8 ? d.K : d.K * 4;
+  g.nch = Q8 ? (d.K + 4095) / 4096 : (d.K + PL * 256 - 1) / (PL * 256);
   const long long G = gridDim.x, bi = blockIdx.x;
   g.i0 = (int)(bi * d.n_items / G);
   g.ni = (int)((bi + 1) * d.n_items / G) - g.i0;
-  g.nslot = g.ni * d.rpi * g.nch;
+  g.nres = g.ni * d.rpi * g.nch;
+  g.nslot = Q8 ? (g.nres + 1) / 2 : g.nres;
   return g;
 }
 
@@ -176,21 +196,117 @@ TL_DEVICE void consume_slot(const PGeo& g, int slot, int lane, const f4 (&buf)[P
   if (lane == 0) res[slot] = a;
 }
 
+// Q8 row R: int8 row and its scale row (runq.c QuantizedTensor, GS = 64).
+TL_DEVICE void q8_row_ptr(const PDesc& d, const PStep& p, int R, const signed char*& q, const float*& sc) {
+  const long long K = d.K;
+  const float* W = d.W0;
+  const float* S = d.S0;
+  long long r = R;
+  if (d.kind == PK_UP) {
+    if (R & 1) { W = d.W1; S = d.S1; }
+    r = R >> 1;
+  } else if (d.kind == PK_QKV) {
+    if (R >= p.dim + p.kvd) { W = d.W2; S = d.S2; r = R - p.dim - p.kvd; }
+    else if (R >= p.dim) { W = d.W1; S = d.S1; r = R - p.dim; }
+  }
+  q = reinterpret_cast<const signed char*>(W) + r * K;
+  sc = S + r * (K >> 6);
+}
+
+// Q8 slot = chunks 2 slot and 2 slot + 1: four 1-KiB wave-loads of int8 each, plus the
+// weight scale of every lane's 16 bytes (one group of 64 spans 4 lanes).  Chunks past the
+// block's end, and bytes past a row's end, are zero-size resources (zeros, no traffic).
+TL_DEVICE void load_slot_q8(const PDesc& d, const PGeo& g, const PStep& p, int slot, int lane, f4 (&buf)[PL],
+                            float (&sc)[PL]) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int Q = 2 * slot + h;
+    const bool qv = Q < g.nres;
+    const int rl = Q / g.nch, c = Q - rl * g.nch;
+    const signed char* row = reinterpret_cast<const signed char*>(d.W0);
+    const float* srow = d.S0;
+    if (qv) q8_row_ptr(d, p, g.i0 * d.rpi + rl, row, srow);
+    const int off = c * 4096;
+    const int left = qv ? g.rowb - off : 0;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<signed char*>(row) + off, (short)0,
+                                                      left > 0 ? left : 0, 0x00020000);
+    const int sleft = qv ? ((g.rowb - off) >> 6) * 4 : 0;
+    const auto ss = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(srow) + (off >> 6), (short)0,
+                                                      sleft > 0 ? sleft : 0, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      buf[h * 4 + u] =
+          __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16 + u * 1024, 0, 2 /*nt*/));
+      sc[h * 4 + u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ss, ((u * 1024 + lane * 16) >> 6) * 4, 0, 0));
+    }
+  }
+}
+
+// Sum over a quad of lanes (the 4 lanes of one 64-wide group), exact in int32.
+TL_DEVICE int quad_sum(int v) {
+  v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  return v;
+}
+
+// runq.c:317-342 per chunk: per group the int32 dot (v_dot4_i32_i8 + quad sum), then
+// val += ((float)ival * w.s) * x.s; chunk sums land in res in chunk order.
+TL_DEVICE void consume_slot_q8(const PGeo& g, int slot, int lane, const f4 (&buf)[PL], const float (&sc)[PL],
+                               const signed char* xq, const float* xsc, float* res) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int Q = 2 * slot + h;
+    const int c = Q % g.nch;
+    float a = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int kb = c * 4096 + u * 1024 + lane * 16;
+      const q8i4 xv = *reinterpret_cast<const q8i4*>(xq + kb);
+      const q8i4 wv = __builtin_bit_cast(q8i4, buf[h * 4 + u]);
+      int dd = __builtin_amdgcn_sdot4(wv.x, xv.x, 0, false);
+      dd = __builtin_amdgcn_sdot4(wv.y, xv.y, dd, false);
+      dd = __builtin_amdgcn_sdot4(wv.z, xv.z, dd, false);
+      dd = __builtin_amdgcn_sdot4(wv.w, xv.w, dd, false);
+      dd = quad_sum(dd);
+      if ((lane & 3) == 0) a += __fmul_rn(__fmul_rn((float)dd, sc[h * 4 + u]), xsc[kb >> 6]);
+    }
+    a = wave_sum(a);
+    if (lane == 0 && Q < g.nres) res[Q] = a;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // Stream this wave's slots (sw, sw + NSW, ...), sw = streaming-wave index; A/B already hold
 // the first two.  Every path loads A and B in the same two places, so the register
 // allocator keeps one pair of register sets for the whole step.
+template <bool Q8>
+TL_DEVICE void load_any(const PDesc& d, const PGeo& g, const PStep& p, int slot, int lane, f4 (&buf)[PL],
+                        float (&sc)[PL]) {
+  if constexpr (Q8) load_slot_q8(d, g, p, slot, lane, buf, sc);
+  else load_slot(d, g, p, slot, lane, buf);
+}
+
+template <bool Q8>
+TL_DEVICE void consume_any(const PGeo& g, int slot, int lane, const f4 (&buf)[PL], const float (&sc)[PL],
+                           const f4* xs, const signed char* xq, const float* xsc, float* res) {
+  if constexpr (Q8) consume_slot_q8(g, slot, lane, buf, sc, xq, xsc, res);
+  else consume_slot(g, slot, lane, buf, xs, res);
+}
+
+template <bool Q8>
 TL_DEVICE void run_gemv(const PDesc& d, const PGeo& g, const PStep& p, int sw, int lane, const f4* xs,
-                        float* res, f4 (&A)[PL], f4 (&B)[PL]) {
+                        const signed char* xq, const float* xsc, float* res, f4 (&A)[PL], f4 (&B)[PL],
+                        float (&SA)[PL], float (&SB)[PL]) {
   const int nk = g.nslot > sw ? (g.nslot - sw + NSW - 1) / NSW : 0;
   // sched_barrier: keep each refill behind the slot's last use (no third register set)
   for (int k = 0; k < nk; k += 2) {
-    consume_slot(g, sw + k * NSW, lane, A, xs, res);
+    consume_any<Q8>(g, sw + k * NSW, lane, A, SA, xs, xq, xsc, res);
     __builtin_amdgcn_sched_barrier(0);
-    load_slot(d, g, p, sw + (k + 2) * NSW, lane, A);
+    load_any<Q8>(d, g, p, sw + (k + 2) * NSW, lane, A, SA);
     __builtin_amdgcn_sched_barrier(0);
-    if (k + 1 < nk) consume_slot(g, sw + (k + 1) * NSW, lane, B, xs, res);
+    if (k + 1 < nk) consume_any<Q8>(g, sw + (k + 1) * NSW, lane, B, SB, xs, xq, xsc, res);
     __builtin_amdgcn_sched_barrier(0);
-    load_slot(d, g, p, sw + (k + 3) * NSW, lane, B);
+    load_any<Q8>(d, g, p, sw + (k + 3) * NSW, lane, B, SB);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -200,9 +316,10 @@ TL_DEVICE void run_gemv(const PDesc& d, const PGeo& g, const PStep& p, int sw, i
 // The input is the previous phase's granules (all issued at once, then re-polled until
 // their tags match), or — QKV at layer 0, or the classifier of a model without layers —
 // the token's embedding row (weights: plain loads).  Ends with a workgroup barrier.
-TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, const float* rmsw, float* red,
-                     int wave, int lane) {
-  const int n4 = d.K >> 2, pad4 = g.nch * PL * 64;
+template <bool Q8>
+TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, signed char* xq, float* xsc,
+                     const float* rmsw, float* red, int wave, int lane) {
+  const int n4 = d.K >> 2, pad4 = Q8 ? n4 : g.nch * PL * 64;
   float sq = 0.f;
   if (!d.gin) {
     const f4* emb = reinterpret_cast<const f4*>(p.emb + (long long)p.tok[0] * p.dim);
@@ -254,6 +371,33 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, cons
       const f4 v = xs[j];
       xs[j] = f4{__fmul_rn(w.x, __fmul_rn(s, v.x)), __fmul_rn(w.y, __fmul_rn(s, v.y)),
                  __fmul_rn(w.z, __fmul_rn(s, v.z)), __fmul_rn(w.w, __fmul_rn(s, v.w))};
+    }
+  }
+  if constexpr (Q8) {
+    // runq.c:145-171 quantize over the padded strip: 4 consecutive threads (one quad) per
+    // group of 64, 16 values each; scale = max|x| / 127, q = round(x / scale)
+    __syncthreads();
+    const int nsl = g.nch * 256;
+    for (int sl = threadIdx.x; sl < nsl; sl += PT) {
+      f4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = sl * 4 + u < n4 ? xs[sl * 4 + u] : f4{0.f, 0.f, 0.f, 0.f};
+      float m = 0.f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+      m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0xB1, 0xF, 0xF, false)));
+      m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0x4E, 0xF, 0xF, false)));
+      const float scale = __fdiv_rn(m, 127.0f);
+      q8i4 packed;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q0 = q8_round(__fdiv_rn(v[u].x, scale)), q1 = q8_round(__fdiv_rn(v[u].y, scale));
+        const int q2 = q8_round(__fdiv_rn(v[u].z, scale)), q3 = q8_round(__fdiv_rn(v[u].w, scale));
+        packed[u] = (q0 & 0xFF) | ((q1 & 0xFF) << 8) | ((q2 & 0xFF) << 16) | ((q3 & 0xFF) << 24);
+      }
+      *reinterpret_cast<q8i4*>(xq + sl * 16) = packed;
+      if ((sl & 3) == 0) xsc[sl >> 2] = scale;
     }
   }
   __syncthreads();
@@ -358,14 +502,14 @@ TL_DEVICE void grid_barrier(const PStep& p) {
 
 // The phase sequence as seen by one wave.  ROLE0 = the control wave (epilogues, attention,
 // norm preloads); the other waves stream.  Both execute the same workgroup barriers.
-template <int HS, bool ROLE0>
+template <int HS, bool ROLE0, bool Q8>
 TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* res, float* xres, float* red,
-                      float* rmsw, f4* xs, unsigned tb) {
+                      float* rmsw, f4* xs, signed char* xq, float* xsc, unsigned tb) {
   const int G = gridDim.x;
   const int nph = 5 * p.L + 1;
   if constexpr (ROLE0) {
     // this block's slice of the residual stream starts as the token's embedding row
-    const PGeo gx = geo(make_desc(p, PK_WO, 0, tb));
+    const PGeo gx = geo<Q8>(make_desc<Q8>(p, PK_WO, 0, tb));
     const float* er = p.emb + (long long)p.tok[0] * p.dim + gx.i0;
     for (int it = lane; it < gx.ni; it += 64) xres[it] = er[it];
     preload_rms(p.L > 0 ? p.rms_att : p.rms_final, p.dim, rmsw, lane);
@@ -391,9 +535,9 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
         TRACE(3);
         continue;
       }
-      const PDesc d = make_desc(p, kind, l, tb);
-      const PGeo g = geo(d);
-      stage(d, g, p, xs, rmsw, red, wave, lane);
+      const PDesc d = make_desc<Q8>(p, kind, l, tb);
+      const PGeo g = geo<Q8>(d);
+      stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, wave, lane);
       TRACE(1);
       if (kind == PK_QKV) preload_rms(p.rms_ffn + (long long)l * p.dim, p.dim, rmsw, lane);
       if (kind == PK_UP) preload_rms(l + 1 < p.L ? p.rms_att + (long long)(l + 1) * p.dim : p.rms_final, p.dim, rmsw, lane);
@@ -405,26 +549,27 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
   } else {
     const int sw = wave - 1;
     f4 A[PL], B[PL];
+    float SA[PL], SB[PL];  // Q8 weight scales (unused for fp32)
     __syncthreads();  // first norm weights preloaded
     {
-      const PDesc d0 = make_desc(p, p.L > 0 ? PK_QKV : PK_CLS, p.L > 0 ? 0 : p.L, tb);
-      const PGeo g0 = geo(d0);
-      load_slot(d0, g0, p, sw, lane, A);
-      load_slot(d0, g0, p, sw + NSW, lane, B);
+      const PDesc d0 = make_desc<Q8>(p, p.L > 0 ? PK_QKV : PK_CLS, p.L > 0 ? 0 : p.L, tb);
+      const PGeo g0 = geo<Q8>(d0);
+      load_any<Q8>(d0, g0, p, sw, lane, A, SA);
+      load_any<Q8>(d0, g0, p, sw + NSW, lane, B, SB);
     }
     for (int ph = 0; ph < nph; ++ph) {
       const int l = ph / 5;
       const int kind = ph == nph - 1 ? PK_CLS : ph % 5;
       if (kind == PK_ATTN) continue;
-      const PDesc d = make_desc(p, kind, kind == PK_CLS ? p.L : l, tb);
-      const PGeo g = geo(d);
-      stage(d, g, p, xs, rmsw, red, wave, lane);
-      run_gemv(d, g, p, sw, lane, xs, res, A, B);
+      const PDesc d = make_desc<Q8>(p, kind, kind == PK_CLS ? p.L : l, tb);
+      const PGeo g = geo<Q8>(d);
+      stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, wave, lane);
+      run_gemv<Q8>(d, g, p, sw, lane, xs, xq, xsc, res, A, B, SA, SB);
       if (kind != PK_CLS) {
-        const PDesc nd = next_desc(p, kind, l, tb);
-        const PGeo ng = geo(nd);
-        load_slot(nd, ng, p, sw, lane, A);
-        load_slot(nd, ng, p, sw + NSW, lane, B);
+        const PDesc nd = next_desc<Q8>(p, kind, l, tb);
+        const PGeo ng = geo<Q8>(nd);
+        load_any<Q8>(nd, ng, p, sw, lane, A, SA);
+        load_any<Q8>(nd, ng, p, sw + NSW, lane, B, SB);
       }
       __syncthreads();  // every slot reduced into res
     }
@@ -457,7 +602,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
   }
 }
 
-template <int HS>
+template <int HS, bool Q8>
 __global__ void __launch_bounds__(PT) persistent_step_kernel(PStep p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* strips = reinterpret_cast<float*>(smem);  // 64: attention score strip of wave 0
@@ -466,15 +611,25 @@ __global__ void __launch_bounds__(PT) persistent_step_kernel(PStep p) {
   float* red = res + kPResFloats;                   // 16: block reductions
   float* rmsw = red + 16;                           // dim: the next norm's weights
   f4* xs = reinterpret_cast<f4*>(rmsw + p.dim);     // pad_floats: the staged input
+  signed char* xq = reinterpret_cast<signed char*>(rmsw + p.dim + p.pad_floats);  // Q8: q8_pad int8
+  float* xsc = reinterpret_cast<float*>(xq + p.q8_pad);                           //     q8_pad/64 scales
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const unsigned tb = p.seq[0] << 12;  // tag base of this launch
-  if (wave == 0) phases<HS, true>(p, wave, lane, strips, res, xres, red, rmsw, xs, tb);
-  else phases<HS, false>(p, wave, lane, strips, res, xres, red, rmsw, xs, tb);
+  if (wave == 0) phases<HS, true, Q8>(p, wave, lane, strips, res, xres, red, rmsw, xs, xq, xsc, tb);
+  else phases<HS, false, Q8>(p, wave, lane, strips, res, xres, red, rmsw, xs, xq, xsc, tb);
 }
 
 static size_t lds_bytes(const PStep& p) {
-  return (size_t)(64 + kPResidFloats + kPResFloats + 16 + p.dim + p.pad_floats) * 4;
+  return (size_t)(64 + kPResidFloats + kPResFloats + 16 + p.dim + p.pad_floats) * 4 + (size_t)p.q8_pad +
+         (size_t)p.q8_pad / 16;
+}
+
+template <int HS, bool Q8>
+static const void* kfn() { return (const void*)persistent_step_kernel<HS, Q8>; }
+static const void* kernel_of(const PStep& p) {
+  if (p.q8) return p.hs == 128 ? kfn<128, true>() : kfn<64, true>();
+  return p.hs == 128 ? kfn<128, false>() : kfn<64, false>();
 }
 
 bool persistent_prepare(PStep& p, int ncu, const char** why) {
@@ -483,14 +638,16 @@ bool persistent_prepare(PStep& p, int ncu, const char** why) {
   if (p.dim % 256 || p.hid % 256) return fail("dim and hidden_dim must be multiples of 256");
   if (p.NS < 1 || p.NS > kMaxNS) return fail("attention splits out of range");
   if (ncu < 8) return fail("too few compute units");
+  if (p.q8 && p.q8 != 64) return fail("int8 group size must be 64");
   if (5 * p.L + 1 >= 4096) return fail("too many layers for the phase tags");
   // every block must own work in every phase: a hand-off buffer may be rewritten as soon as
   // the next phase's outputs are complete, which then implies every block has staged it
   if (p.dim < ncu || (p.dim + 2 * p.kvd) / 2 < ncu || p.hid < ncu) return fail("model too small for the grid");
-  auto nchunks = [](int K) { return (K + PL * 256 - 1) / (PL * 256); };
-  auto padf = [&](int K) { return nchunks(K) * PL * 256; };
+  auto nchunks = [&](int K) { return p.q8 ? (K + 4095) / 4096 : (K + PL * 256 - 1) / (PL * 256); };
+  auto padf = [&](int K) { return p.q8 ? K : nchunks(K) * PL * 256; };
   auto nrc = [&](int K, int n_items, int rpi) { return ((n_items + ncu - 1) / ncu) * rpi * nchunks(K); };
   p.pad_floats = padf(p.dim) > padf(p.hid) ? padf(p.dim) : padf(p.hid);
+  p.q8_pad = p.q8 ? 4096 * (nchunks(p.dim) > nchunks(p.hid) ? nchunks(p.dim) : nchunks(p.hid)) : 0;
   if (nrc(p.dim, (p.dim + 2 * p.kvd) / 2, 2) > kPResFloats || nrc(p.dim, p.hid, 2) > kPResFloats ||
       nrc(p.hid, p.dim, 1) > kPResFloats || nrc(p.dim, p.V, 1) > kPResFloats)
     return fail("too many rows per block");
@@ -498,27 +655,26 @@ bool persistent_prepare(PStep& p, int ncu, const char** why) {
   if (lds_bytes(p) > 160 * 1024) return fail("activations do not fit the LDS");
   static bool attr_set = false;
   if (!attr_set) {  // allow more than 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
-    if (hipFuncSetAttribute((const void*)persistent_step_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024) != hipSuccess ||
-        hipFuncSetAttribute((const void*)persistent_step_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024) != hipSuccess)
-      return fail("cannot raise the dynamic LDS limit");
+    for (const void* f : {kfn<128, false>(), kfn<64, false>(), kfn<128, true>(), kfn<64, true>()})
+      if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+        return fail("cannot raise the dynamic LDS limit");
     attr_set = true;
   }
   int nb = 0;
-  const hipError_t e = p.hs == 128
-      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, persistent_step_kernel<128>, PT, lds_bytes(p))
-      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, persistent_step_kernel<64>, PT, lds_bytes(p));
+  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel_of(p), PT, lds_bytes(p));
   if (e != hipSuccess || nb < 1) return fail("persistent kernel does not fit one block per CU");
   return true;
 }
 
 // The caller zeroes p.sync (kPSyncWords) and the tickets on the same stream right before.
 hipError_t launch_persistent_step(const PStep& p, hipStream_t s, int ncu) {
-  if (p.hs == 128)
-    hipLaunchKernelGGL(persistent_step_kernel<128>, dim3(ncu), dim3(PT), lds_bytes(p), s, p);
-  else
-    hipLaunchKernelGGL(persistent_step_kernel<64>, dim3(ncu), dim3(PT), lds_bytes(p), s, p);
+  if (p.q8) {
+    if (p.hs == 128) hipLaunchKernelGGL((persistent_step_kernel<128, true>), dim3(ncu), dim3(PT), lds_bytes(p), s, p);
+    else hipLaunchKernelGGL((persistent_step_kernel<64, true>), dim3(ncu), dim3(PT), lds_bytes(p), s, p);
+  } else {
+    if (p.hs == 128) hipLaunchKernelGGL((persistent_step_kernel<128, false>), dim3(ncu), dim3(PT), lds_bytes(p), s, p);
+    else hipLaunchKernelGGL((persistent_step_kernel<64, false>), dim3(ncu), dim3(PT), lds_bytes(p), s, p);
+  }
   return hipGetLastError();
 }
 

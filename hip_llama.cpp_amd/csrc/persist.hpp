@@ -1,4 +1,4 @@
-// persist.hpp — the one-launch decode step (persist.hip) for batch 1, fp32 weights.
+// persist.hpp — the one-launch decode step (persist.hip) for batch 1, fp32 or Q8_0 weights.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -24,6 +24,15 @@ struct PStep {
   int argmax;               // run the argmax + advance tail
   int pad_floats;           // LDS activation strip (floats), >= every phase's padded K
   unsigned long long* trace; // optional [grid][5L+1][4] timeline (100-MHz clock), or null
+  // Q8_0 weights (runq.c layout, include/thaQ8.hpp) instead of the fp32 matrices: group size
+  // (64; 0 = fp32) and a device table of per-layer (int8, scale) addresses for wq, wk, wv,
+  // wo, w1, w2, w3 ([7][L][2]); the classifier's pair separately.  Norms and the (dequantised)
+  // embedding stay fp32 in the fields above.
+  int q8;
+  const unsigned long long* q8tab;
+  const signed char* qcls;
+  const float* scls;
+  int q8_pad;               // LDS bytes of the quantised activation strip (Q8 only)
 };
 
 constexpr int kPSyncWords = 8 * 32;   // 8 shard counters, one 128-B line each

@@ -473,4 +473,8 @@ def step_bytes_q8(cfg, batch, kclass, pos, gs):
         return qt(hid * dim) + 4 * batch * (hid + 2 * dim)
     if kclass == K_CLS:
         return qt(V * dim) + 4 * (dim + batch * (dim + V))
+    if kclass == K_STEP:  # the persistent step: every class of the step in one launch
+        per_layer = sum(step_bytes_q8(cfg, batch, k, pos, gs) for k in (K_QKV, K_ATTN, K_WO, K_FFN_UP, K_FFN_DOWN))
+        return (cfg.n_layers * per_layer + step_bytes_q8(cfg, batch, K_CLS, pos, gs)
+                + step_bytes_q8(cfg, batch, K_ARGMAX, pos, gs))
     return step_bytes(cfg, batch, kclass, pos)

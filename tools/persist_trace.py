@@ -28,12 +28,15 @@ def main():
     ap.add_argument("--model", default="7b", choices=sorted(MODELS))
     ap.add_argument("--pos", type=int, default=8, help="position of the traced step")
     ap.add_argument("--json", default="")
+    ap.add_argument("--dtype", default="f32", choices=["f32", "int8"])
     args = ap.parse_args()
     _pkg()
     from hip_llama_cpp_amd import thallama as tl
     cfg = MODELS[args.model]
     c = tl.Config.make(*cfg)
     model = tl.DeviceModel(c, 0, seed=7)
+    if args.dtype == "int8":
+        model = tl.DeviceModelQ8(c, 0, 64, from_model=model)
     state = tl.DeviceState(c, 1)
     dec = tl.Decoder(model, state)
     assert dec.persistent()
@@ -47,8 +50,9 @@ def main():
     t = t.reshape(G, nph, 4)
     t = (t - t[:, 0, 0].min()) * 0.01  # us
     dim, hid, kvd, V = cfg[0], cfg[1], cfg[0] * cfg[4] // cfg[3], cfg[5]
-    wbytes = {"qkv": 4 * dim * (dim + 2 * kvd), "attn": 0, "wo": 4 * dim * dim, "ffn_up": 8 * dim * hid,
-              "ffn_down": 4 * dim * hid, "cls": 4 * dim * V}
+    esz = 4 if args.dtype == "f32" else 1 + 4 / 64  # int8 + one fp32 scale per 64
+    wbytes = {k: v * esz for k, v in {"qkv": dim * (dim + 2 * kvd), "attn": 0, "wo": dim * dim, "ffn_up": 2 * dim * hid,
+                                       "ffn_down": dim * hid, "cls": dim * V}.items()}
     rows = {}
     for ph in range(nph):
         kind = "cls" if ph == nph - 1 else KINDS[ph % 5]
