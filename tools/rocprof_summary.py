@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Summaries of rocprofv3 (ROCm 7.x, SQLite output) runs for profiles/.
+
+    python tools/rocprof_summary.py stats <results.db> <out.csv>
+        kernel, calls, total_us, avg_us, percent  (the top_kernels view of --kernel-trace --stats)
+    python tools/rocprof_summary.py pmc <fetch_results.db> <write_results.db> <out.json> [note]
+        per-kernel launch averages of FETCH_SIZE / WRITE_SIZE (separate --pmc passes) and
+        traffic_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (gfx950: FETCH_SIZE counts half of
+        the bytes of wide coalesced streaming reads, MI355X_MICROARCH.md HBM section)
+"""
+import csv
+import json
+import sqlite3
+import sys
+
+
+def stats(db, out):
+    con = sqlite3.connect(db)
+    rows = con.execute("select name, total_calls, total_duration, average, percentage from top_kernels "
+                       "order by total_duration desc").fetchall()
+    with open(out, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["kernel", "calls", "total_us", "avg_us", "percent"])
+        for name, calls, tot, avg, pct in rows:
+            w.writerow([name, calls, round(tot, 3), round(avg, 3), round(pct, 3)])  # top_kernels: us
+
+
+def counter(db, name):
+    con = sqlite3.connect(db)
+    acc = {}
+    for kname, val in con.execute("select kernel_name, value from counters_collection where counter_name = ?",
+                                  (name,)):
+        s = acc.setdefault(kname, [0.0, 0])
+        s[0] += val
+        s[1] += 1
+    return {k: (v[0] / v[1], v[1]) for k, v in acc.items()}
+
+
+def pmc(fetch_db, write_db, out, note=""):
+    fe, wr = counter(fetch_db, "FETCH_SIZE"), counter(write_db, "WRITE_SIZE")
+    res = {}
+    for k, (f, n) in fe.items():
+        w = wr.get(k, (0.0, 0))[0]
+        res[k] = {"launches": n, "FETCH_SIZE_KB_avg": f, "WRITE_SIZE_KB_avg": w,
+                  "traffic_bytes": 2 * f * 1024 + w * 1024}
+    with open(out, "w") as fo:
+        json.dump({"_how": note, "kernels": res}, fo, indent=1)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "stats":
+        stats(sys.argv[2], sys.argv[3])
+    else:
+        pmc(sys.argv[2], sys.argv[3], sys.argv[4], sys.argv[5] if len(sys.argv) > 5 else "")
