@@ -21,8 +21,8 @@ __device__ inline float wsum(float v) {
   return v;
 }
 
-template <int NC, int NSLOT, int DEPTH>
-__global__ void __launch_bounds__((NC + 1) * 64) ring_kernel(const float* W, int slots_per_cu, const float* x, float* out) {
+template <int NC, int NSLOT, int DEPTH, int NL>
+__global__ void __launch_bounds__((NC + NL) * 64) ring_kernel(const float* W, int slots_per_cu, const float* x, float* out) {
   __shared__ __attribute__((aligned(16))) float ring[NSLOT][SLOTF];
   __shared__ __attribute__((aligned(16))) float xs[SLOTF];
   __shared__ unsigned full[NSLOT], freed[NSLOT];
@@ -32,9 +32,10 @@ __global__ void __launch_bounds__((NC + 1) * 64) ring_kernel(const float* W, int
   if (threadIdx.x < NSLOT) { full[threadIdx.x] = 0; freed[threadIdx.x] = 0; }
   __syncthreads();
   const float* base = W + (size_t)blockIdx.x * slots_per_cu * SLOTF;
-  if (wave == 0) {
-    // loader
-    for (int s = 0; s < slots_per_cu + DEPTH - 1; ++s) {
+  if (wave < NL) {
+    // loader wave `wave`: slots wave, wave + NL, ...; DEPTH of its own slots in flight
+    for (int j = 0; j * NL + wave < slots_per_cu + (DEPTH - 1) * NL; ++j) {
+      const int s = j * NL + wave;
       if (s < slots_per_cu) {
         const int slot = s % NSLOT;
         const unsigned gen = s / NSLOT;  // times this slot was filled before
@@ -46,9 +47,9 @@ __global__ void __launch_bounds__((NC + 1) * 64) ring_kernel(const float* W, int
           __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + i * 256 + lane * 4),
                                            (__attribute__((address_space(3))) void*)(&ring[slot][i * 256]), 16, 0, 2);
       }
-      // publish slot s - DEPTH + 1 once its 16 loads have landed
-      const int ps = s - DEPTH + 1;
-      if (ps >= 0) {
+      // publish this wave's slot DEPTH - 1 back once its 16 loads have landed
+      const int ps = s - (DEPTH - 1) * NL;
+      if (ps >= 0 && ps < slots_per_cu) {
         if (s < slots_per_cu) {
           if constexpr (DEPTH == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           else if constexpr (DEPTH == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
@@ -61,7 +62,7 @@ __global__ void __launch_bounds__((NC + 1) * 64) ring_kernel(const float* W, int
       }
     }
   } else {
-    const int c = wave - 1;
+    const int c = wave - NL;
     float acc = 0.f;
     for (int s = c; s < slots_per_cu; s += NC) {
       const int slot = s % NSLOT;
@@ -117,9 +118,9 @@ __global__ void __launch_bounds__(512) reg_kernel(const float* W, int slots_per_
   if (lane == 0) out[blockIdx.x * 16 + wave] = acc;
 }
 
-template <int NC, int NSLOT, int DEPTH>
+template <int NC, int NSLOT, int DEPTH, int NL = 1>
 static void launch_ring(int ncu, const float* W, int spc, const float* x, float* out) {
-  hipLaunchKernelGGL((ring_kernel<NC, NSLOT, DEPTH>), dim3(ncu), dim3((NC + 1) * 64), 0, 0, W, spc, x, out);
+  hipLaunchKernelGGL((ring_kernel<NC, NSLOT, DEPTH, NL>), dim3(ncu), dim3((NC + NL) * 64), 0, 0, W, spc, x, out);
 }
 
 template <class F>
@@ -155,12 +156,12 @@ int main() {
     printf("%-28s %8.2f us  %7.0f GB/s\n", NAME, ms * 1e3, bytes / (ms * 1e-3) / 1e9);         \
   }
   RUN("register 8w 2x8KiB", hipLaunchKernelGGL(reg_kernel, dim3(ncu), dim3(512), 0, 0, Wc, spc, x, out));
-  RUN("ring 3c 6slot depth2", launch_ring<3, 6, 2>(ncu, Wc, spc, x, out));
-  RUN("ring 3c 6slot depth3", launch_ring<3, 6, 3>(ncu, Wc, spc, x, out));
-  RUN("ring 4c 6slot depth3", launch_ring<4, 6, 3>(ncu, Wc, spc, x, out));
-  RUN("ring 4c 8slot depth4", launch_ring<4, 8, 4>(ncu, Wc, spc, x, out));
-  RUN("ring 6c 8slot depth4", launch_ring<6, 8, 4>(ncu, Wc, spc, x, out));
-  RUN("ring 3c 5slot depth3", launch_ring<3, 5, 3>(ncu, Wc, spc, x, out));
+  RUN("ring 3c 6slot d3 1L", launch_ring<3, 6, 3, 1>(ncu, Wc, spc, x, out));
+  RUN("ring 4c 8slot d2 2L", launch_ring<4, 8, 2, 2>(ncu, Wc, spc, x, out));
+  RUN("ring 4c 8slot d3 2L", launch_ring<4, 8, 3, 2>(ncu, Wc, spc, x, out));
+  RUN("ring 4c 8slot d2 4L", launch_ring<4, 8, 2, 4>(ncu, Wc, spc, x, out));
+  RUN("ring 6c 8slot d1 4L", launch_ring<6, 8, 1, 4>(ncu, Wc, spc, x, out));
+  RUN("ring 4c 6slot d1 4L", launch_ring<4, 6, 1, 4>(ncu, Wc, spc, x, out));
   RUN("register 8w 2x8KiB", hipLaunchKernelGGL(reg_kernel, dim3(ncu), dim3(512), 0, 0, Wc, spc, x, out));
   CK(hipGetLastError());
   CK(hipDeviceSynchronize());
