@@ -48,7 +48,7 @@ def main():
     ap.add_argument("--no-nt", action="store_true")
     ap.add_argument("--splits", type=int, default=0)
     ap.add_argument("--no-persistent", action="store_true",
-                    help="multi-launch step instead of the one-launch persistent step (batch 1 fp32)")
+                    help="multi-launch step instead of the one-launch persistent step (batch 1)")
     ap.add_argument("--cpu-baseline-tokens", type=int, default=2)
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--prof-steps", type=int, default=16)
