@@ -142,7 +142,8 @@ struct thallama_decoder {
   size_t psync_zero = 0;        // words zeroed before every launch
   unsigned long long* pbmax = nullptr;
   unsigned long long* pgran = nullptr;  // hand-off granules: x | xb | hb | qkv
-  unsigned long long* pq8tab = nullptr; // int8: per-layer (int8, scale) addresses [7][L][2]
+  const signed char* pq8w[7] = {};       // int8: layer-0 int8 block of wq wk wv wo w1 w2 w3
+  long long pq8ls[7] = {};                // and the byte stride between layers
   bool pok = false;             // shape supported
   unsigned long long* ptrace = nullptr;  // optional timeline of the persistent step
   size_t ptrace_n = 0;
@@ -317,7 +318,6 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   (void)hipFree(d->psync);
   (void)hipFree(d->pbmax);
   (void)hipFree(d->pgran);
-  (void)hipFree(d->pq8tab);
   (void)hipFree(d->ptrace);
   for (void* b : {(void*)d->pf_x, (void*)d->pf_xn, (void*)d->pf_q, (void*)d->pf_xb, (void*)d->pf_hb,
                   (void*)d->pf_part, (void*)d->pf_cnt, (void*)d->pf_tok, (void*)d->pf_pos})
@@ -562,7 +562,10 @@ static int enqueue_persistent(thallama_decoder* d, bool argmax) {
   p.trace = d->ptrace;
   if (d->q8) {
     p.q8 = d->w8.group_size;
-    p.q8tab = d->pq8tab;
+    for (int t = 0; t < 7; ++t) {
+      p.q8w[t] = d->pq8w[t];
+      p.q8ls[t] = d->pq8ls[t];
+    }
     p.qcls = d->w8.wcls->q;
     p.scls = d->w8.wcls->s;
   }
@@ -834,15 +837,30 @@ extern "C" int thallama_decoder_create_q8(thallama_decoder** out, const Config* 
     if (!d->pok && why) d->pwhy = why;
   }
   if (d->pok) {
+    // the kernel addresses layer l of tensor t as q(0) + l * stride with the scales right
+    // after each int8 block (the v2 payload order, thallama_q8_map); anything else -> the
+    // multi-launch int8 step
     const QuantizedTensor* ts[7] = {w8->wq, w8->wk, w8->wv, w8->wo, w8->w1, w8->w2, w8->w3};
-    std::vector<unsigned long long> tab((size_t)7 * d->L * 2);
-    for (int t = 0; t < 7; ++t)
+    const long long dim = d->dim, kvd = d->kv_dim, hid = d->hidden;
+    const long long nel[7] = {dim * dim, kvd * dim, kvd * dim, dim * dim, hid * dim, dim * hid, hid * dim};
+    for (int t = 0; t < 7 && d->pok; ++t) {
+      const signed char* b = (const signed char*)ts[t][0].q;
+      const long long stride = d->L > 1 ? (const signed char*)ts[t][1].q - b : 0;
       for (int l = 0; l < d->L; ++l) {
-        tab[((size_t)t * d->L + l) * 2] = (unsigned long long)(uintptr_t)ts[t][l].q;
-        tab[((size_t)t * d->L + l) * 2 + 1] = (unsigned long long)(uintptr_t)ts[t][l].s;
+        const signed char* q = (const signed char*)ts[t][l].q;
+        if (q != b + l * stride || (const signed char*)ts[t][l].s != q + nel[t]) {
+          d->pok = false;
+          d->pwhy = "int8 tensors not in the v2 payload layout";
+          break;
+        }
       }
-    TL_TRY(hipMalloc(&d->pq8tab, sizeof(unsigned long long) * (tab.size() > 0 ? tab.size() : 1)));
-    TL_TRY(hipMemcpy(d->pq8tab, tab.data(), sizeof(unsigned long long) * tab.size(), hipMemcpyHostToDevice));
+      d->pq8w[t] = b;
+      d->pq8ls[t] = stride;
+    }
+    if ((const signed char*)w8->wcls->s != (const signed char*)w8->wcls->q + (long long)d->V * dim) {
+      d->pok = false;
+      d->pwhy = "int8 classifier not in the v2 payload layout";
+    }
   }
   return 0;
 }

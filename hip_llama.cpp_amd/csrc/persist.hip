@@ -98,15 +98,25 @@ TL_DEVICE PDesc make_desc(const PStep& p, int kind, int l, unsigned tb) {
       break;
   }
   if constexpr (Q8) {
-    // per-layer (int8, scale) pairs: table [tensor][L][2], tensors wq wk wv wo w1 w2 w3
-    auto q = [&](int t, int i) { return reinterpret_cast<const float*>(p.q8tab[((long long)t * p.L + l) * 2 + i]); };
-    switch (kind) {
-      case PK_QKV: d.W0 = q(0, 0); d.S0 = q(0, 1); d.W1 = q(1, 0); d.S1 = q(1, 1); d.W2 = q(2, 0); d.S2 = q(2, 1); break;
-      case PK_WO: d.W0 = q(3, 0); d.S0 = q(3, 1); break;
-      case PK_UP: d.W0 = q(4, 0); d.S0 = q(4, 1); d.W1 = q(6, 0); d.S1 = q(6, 1); break;
-      case PK_DOWN: d.W0 = q(5, 0); d.S0 = q(5, 1); break;
-      default: d.W0 = reinterpret_cast<const float*>(p.qcls); d.S0 = p.scls; break;
-    }
+    // tensor t of layer l: int8 block at q8w[t] + l * q8ls[t], its rows x K scales after it.
+    // Tensor ids and shapes are picked as scalars and every field is assigned once: per-arm
+    // field stores were merged into stores through a phi of stack slots (scratch traffic).
+    // QKV: wq wk wv | WO: wo | UP: w1, w3 | DOWN: w2 | CLS: the classifier pair
+    const int t0 = kind == PK_QKV ? 0 : kind == PK_WO ? 3 : kind == PK_UP ? 4 : 5;
+    const int t1 = kind == PK_UP ? 6 : 1;
+    const long long rows0 = kind == PK_QKV || kind == PK_WO || kind == PK_DOWN ? dim : hid;
+    const long long rows1 = kind == PK_UP ? hid : kvd;
+    const long long K0 = kind == PK_DOWN ? hid : dim;
+    const signed char* b0 = p.q8w[t0] + ll * p.q8ls[t0];
+    const signed char* b1 = p.q8w[t1] + ll * p.q8ls[t1];
+    const signed char* b2 = p.q8w[2] + ll * p.q8ls[2];
+    const bool cls = kind == PK_CLS;
+    d.W0 = reinterpret_cast<const float*>(cls ? p.qcls : b0);
+    d.S0 = cls ? p.scls : reinterpret_cast<const float*>(b0 + rows0 * K0);
+    d.W1 = reinterpret_cast<const float*>(b1);
+    d.S1 = reinterpret_cast<const float*>(b1 + rows1 * dim);
+    d.W2 = reinterpret_cast<const float*>(b2);
+    d.S2 = reinterpret_cast<const float*>(b2 + kvd * dim);
   }
   return d;
 }
@@ -196,21 +206,31 @@ TL_DEVICE void consume_slot(const PGeo& g, int slot, int lane, const f4 (&buf)[P
   if (lane == 0) res[slot] = a;
 }
 
-// Q8 row R: int8 row and its scale row (runq.c QuantizedTensor, GS = 64).
-TL_DEVICE void q8_row_ptr(const PDesc& d, const PStep& p, int R, const signed char*& q, const float*& sc) {
+// Q8 row R: int8 row and its scale row (runq.c QuantizedTensor, GS = 64).  Returned by value
+// and chosen by integer arithmetic: reference out-parameters behind a condition became a phi
+// of stack slots (scratch traffic in the streaming loop).
+struct Q8Row {
+  const signed char* q;
+  const float* s;
+};
+
+TL_DEVICE Q8Row q8_row_ptr(const PDesc& d, const PStep& p, int R) {
   const long long K = d.K;
-  const float* W = d.W0;
-  const float* S = d.S0;
+  int m = 0;
   long long r = R;
   if (d.kind == PK_UP) {
-    if (R & 1) { W = d.W1; S = d.S1; }
+    m = R & 1;
     r = R >> 1;
   } else if (d.kind == PK_QKV) {
-    if (R >= p.dim + p.kvd) { W = d.W2; S = d.S2; r = R - p.dim - p.kvd; }
-    else if (R >= p.dim) { W = d.W1; S = d.S1; r = R - p.dim; }
+    if (R >= p.dim + p.kvd) { m = 2; r = R - p.dim - p.kvd; }
+    else if (R >= p.dim) { m = 1; r = R - p.dim; }
   }
-  q = reinterpret_cast<const signed char*>(W) + r * K;
-  sc = S + r * (K >> 6);
+  const unsigned long long w0 = (unsigned long long)d.W0, s0 = (unsigned long long)d.S0;
+  const unsigned long long W = w0 + (m == 1 ? (unsigned long long)d.W1 - w0 : 0ull) +
+                               (m == 2 ? (unsigned long long)d.W2 - w0 : 0ull);
+  const unsigned long long S = s0 + (m == 1 ? (unsigned long long)d.S1 - s0 : 0ull) +
+                               (m == 2 ? (unsigned long long)d.S2 - s0 : 0ull);
+  return Q8Row{reinterpret_cast<const signed char*>(W) + r * K, reinterpret_cast<const float*>(S) + r * (K >> 6)};
 }
 
 // Q8 slot = chunks 2 slot and 2 slot + 1: four 1-KiB wave-loads of int8 each, plus the
@@ -223,9 +243,9 @@ TL_DEVICE void load_slot_q8(const PDesc& d, const PGeo& g, const PStep& p, int s
     const int Q = 2 * slot + h;
     const bool qv = Q < g.nres;
     const int rl = Q / g.nch, c = Q - rl * g.nch;
-    const signed char* row = reinterpret_cast<const signed char*>(d.W0);
-    const float* srow = d.S0;
-    if (qv) q8_row_ptr(d, p, g.i0 * d.rpi + rl, row, srow);
+    const Q8Row qr = q8_row_ptr(d, p, qv ? g.i0 * d.rpi + rl : 0);
+    const signed char* row = qr.q;
+    const float* srow = qr.s;
     const int off = c * 4096;
     const int left = qv ? g.rowb - off : 0;
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<signed char*>(row) + off, (short)0,

@@ -25,11 +25,14 @@ struct PStep {
   int pad_floats;           // LDS activation strip (floats), >= every phase's padded K
   unsigned long long* trace; // optional [grid][5L+1][4] timeline (100-MHz clock), or null
   // Q8_0 weights (runq.c layout, include/thaQ8.hpp) instead of the fp32 matrices: group size
-  // (64; 0 = fp32) and a device table of per-layer (int8, scale) addresses for wq, wk, wv,
-  // wo, w1, w2, w3 ([7][L][2]); the classifier's pair separately.  Norms and the (dequantised)
-  // embedding stay fp32 in the fields above.
+  // (64; 0 = fp32); per tensor (wq, wk, wv, wo, w1, w2, w3) the layer-0 int8 block and the
+  // byte stride between layers, each layer's fp32 scales directly after its int8 block (the
+  // v2 payload order; the host checks it); the classifier's pair separately.  Norms and the
+  // (dequantised) embedding stay fp32 in the fields above.  Plain arguments, so every
+  // per-phase address is scalar arithmetic (a device table read put them in VGPRs / scratch).
   int q8;
-  const unsigned long long* q8tab;
+  const signed char* q8w[7];
+  long long q8ls[7];
   const signed char* qcls;
   const float* scls;
   int q8_pad;               // LDS bytes of the quantised activation strip (Q8 only)

@@ -1,0 +1,8 @@
+set -o pipefail
+export TMPDIR=/tmp
+timeout -k 10 600 python -m pytest tests/test_q8_persist_gpu.py tests/test_q8_gpu.py tests/test_persist_gpu.py tests/test_cli_gpu.py -q -x > gpurun_out/q8w.log 2>&1 || { echo "TESTS rc=$?"; tail -40 gpurun_out/q8w.log; exit 1; }
+tail -1 gpurun_out/q8w.log
+timeout -k 10 300 python bench.py --dtype int8 --steps 64 --warmup 4 --skip-cpu > gpurun_out/bq8.log 2>&1 || { echo "bench rc=$?"; tail -20 gpurun_out/bq8.log; exit 1; }
+tail -1 gpurun_out/bq8.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline']['avg_us'])"
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcw_q8 -o pmcw -- python bench.py --steps 4 --warmup 1 --skip-cpu --prof-steps 2 --dtype int8 > gpurun_out/pmcw_q8.out 2>&1 || { echo "pmc rc=$?"; exit 1; }
+echo done
