@@ -904,6 +904,38 @@ extern "C" thablasStatus_t thaDNN_q8_forward_batch(thablasHandle_t handle, int n
 // step starts from the token after the prefilled ones.  fp32 weights, head size 64/128/256.
 static constexpr int kPrefillChunk = 128;
 
+// A prefill projection.  Up to kPrefillGemvMax tokens the decode GEMV (matrix cores from 4
+// tokens on: gemv_mfma.hpp, ~4.5 TB/s) beats the GEMM, whose grid is only M/128 blocks at
+// one 64-token tile (7B: 32-172 blocks, ~1 TB/s); the same epilogues either way.
+static constexpr int kPrefillGemvMax = 16;
+static constexpr int kPrefillGemmMin = 80;
+static hipError_t prefill_proj(thallama_decoder* d, int mode, const tl::PGemmArgs& g, long long kv_l_off) {
+  if (g.n > kPrefillGemvMax) return tl::prefill_gemm(mode, g, d->stream);
+  if (!d->mpart_d) {  // split-K scratch of the matrix-core GEMV (decoders of batch >= 2 have it)
+    const size_t nblk = (size_t)tl::mfma_target_blocks();
+    hipError_t e = hipMalloc(&d->mpart_d, sizeof(float) * nblk * 2 * 256);
+    if (e == hipSuccess) e = hipMalloc(&d->mcnt_d, sizeof(unsigned) * nblk);
+    if (e == hipSuccess) e = hipMemset(d->mcnt_d, 0, sizeof(unsigned) * nblk);
+    if (e != hipSuccess) return e;
+  }
+  tl::GemvParams p = {};
+  p.W0 = g.W0; p.W1 = g.W1; p.W2 = g.W2;
+  p.K = g.K;
+  p.nb = g.n;
+  p.x = g.X; p.x_stride = g.ldx;
+  p.y = g.Y; p.y_stride = g.ldy;
+  p.pos = d->pf_pos;
+  if (mode == tl::GM_QKV) {
+    p.n_items = g.M / 2;
+    p.kc = g.kc - kv_l_off; p.vc = g.vc - kv_l_off;  // one sequence: no batch stride
+    p.kv_b_stride = 0; p.kv_l_off = kv_l_off;
+    p.dim = g.dim; p.kv_dim = g.kv_dim; p.head_size = g.head_size; p.rope = g.rope;
+  } else {
+    p.n_items = mode == tl::GM_SWIGLU ? g.M / 2 : g.M;
+  }
+  return gemv(d, mode, p, nullptr, nullptr, nullptr);
+}
+
 extern "C" int thallama_decoder_prefill(thallama_decoder* d, int b, const int* tokens_h, int n, int pos0) {
   if (!d || !tokens_h || n < 0 || b < 0 || b >= d->B || pos0 < 0 || pos0 + n > d->S) {
     g_last_error = "thallama_decoder_prefill: invalid argument";
@@ -938,8 +970,12 @@ extern "C" int thallama_decoder_prefill(thallama_decoder* d, int b, const int* t
   float* kc_b = d->s.key_cache + (long long)b * kv_b_stride;
   float* vc_b = d->s.value_cache + (long long)b * kv_b_stride;
   hipStream_t st = d->stream;
-  for (int c = 0; c < n; c += CH) {
-    const int m = n - c < CH ? n - c : CH;
+  for (int c = 0, m = 0; c < n; c += m) {
+    // GEMM chunks of up to CH tokens; a rest of at most kPrefillGemmMin tokens goes through
+    // the decode GEMV 16 tokens at a time (about 6 ms per 16 at 7B, against a GEMM floor of
+    // about 31 ms for any chunk up to 64 tokens: tools/prefill_bench.py)
+    const int rest = n - c;
+    m = rest > kPrefillGemmMin ? (rest < CH ? rest : CH) : (rest < kPrefillGemvMax ? rest : kPrefillGemvMax);
     const int p0 = pos0 + c;
     TL_TRY(hipMemcpyAsync(d->pf_tok, tokens_h + c, sizeof(int) * m, hipMemcpyHostToDevice, st));
     TL_TRY(tl::prefill_positions(d->pf_pos, p0, m, st));
@@ -955,7 +991,7 @@ extern "C" int thallama_decoder_prefill(thallama_decoder* d, int b, const int* t
       g.W0 = w.wq + ll * dim * dim; g.W1 = w.wk + ll * dim * kvd; g.W2 = w.wv + ll * dim * kvd;
       g.Y = d->pf_q; g.ldy = dim;
       g.kc = kc_b + ll * S * kvd; g.vc = vc_b + ll * S * kvd;
-      TL_TRY(tl::prefill_gemm(tl::GM_QKV, g, st));
+      TL_TRY(prefill_proj(d, tl::GM_QKV, g, ll * S * kvd));
       // causal attention: the chunk's m positions as "sequences" over this sequence's cache
       {
         tl::AttnWaveParams wp = {};
@@ -979,15 +1015,15 @@ extern "C" int thallama_decoder_prefill(thallama_decoder* d, int b, const int* t
       }
       // Wo + residual
       g.X = d->pf_xb; g.ldx = dim; g.K = dim; g.M = dim; g.W0 = w.wo + ll * dim * dim; g.Y = d->pf_x; g.ldy = dim;
-      TL_TRY(tl::prefill_gemm(tl::GM_RESID, g, st));
+      TL_TRY(prefill_proj(d, tl::GM_RESID, g, 0));
       // RMSNorm + W1/W3 + SwiGLU
       TL_TRY(tl::prefill_rmsnorm(d->pf_xn, d->pf_x, w.rms_ffn_weight + ll * dim, m, dim, st));
       g.X = d->pf_xn; g.ldx = dim; g.K = dim; g.M = 2 * hid;
       g.W0 = w.w1 + ll * dim * hid; g.W1 = w.w3 + ll * dim * hid; g.Y = d->pf_hb; g.ldy = hid;
-      TL_TRY(tl::prefill_gemm(tl::GM_SWIGLU, g, st));
+      TL_TRY(prefill_proj(d, tl::GM_SWIGLU, g, 0));
       // W2 + residual
       g.X = d->pf_hb; g.ldx = hid; g.K = hid; g.M = dim; g.W0 = w.w2 + ll * dim * hid; g.Y = d->pf_x; g.ldy = dim;
-      TL_TRY(tl::prefill_gemm(tl::GM_RESID, g, st));
+      TL_TRY(prefill_proj(d, tl::GM_RESID, g, 0));
     }
   }
   TL_TRY(hipStreamSynchronize(st));
