@@ -67,6 +67,7 @@ static void error_usage() {
   fprintf(stderr, "  -f <string> (only for test mode) input filename\n");
   fprintf(stderr, "  -o <string> (only for test mode) output filename\n");
   fprintf(stderr, "  -b <string> batch size\n");
+  fprintf(stderr, "  -g <int>    (test mode, not in the reference) 1 = greedy decoding instead of T=1.0/top-p 0.9\n");
   exit(EXIT_FAILURE);
 }
 
@@ -289,7 +290,7 @@ int main(int argc, char* argv[]) {
   char* checkpoint_path = nullptr;
   const char* tokenizer_path = "./assets/tokenizer.bin";
   float temperature = 1.0f, topp = 0.9f;
-  int steps = 256, batch = 1;
+  int steps = 256, batch = 1, greedy_test = 0;
   const char* prompt = nullptr;
   unsigned long long rng_seed = 0;
   const char* mode = "generate";
@@ -313,6 +314,7 @@ int main(int argc, char* argv[]) {
       case 'f': input_filename = v; break;
       case 'o': output_filename = v; break;
       case 'b': batch = atoi(v); break;
+      case 'g': greedy_test = atoi(v); break;
       default: error_usage();
     }
   }
@@ -349,6 +351,7 @@ int main(int argc, char* argv[]) {
       fprintf(stderr, "cannot open the file: %s\n", input_filename);
       exit(EXIT_FAILURE);
     }
+    if (greedy_test) thallama_requests_set_sampling(req, 0.0f, 0.9f);
     printf("requests size = %lu B\n",
            (unsigned long)(((size_t)thallama_requests_count(req) * max_token_len * steps + 1) * 2));
     int n_dev = 0;

@@ -42,6 +42,7 @@ def lib():
             "thallama_random_f32": (F, [C.POINTER(ULL)]),
             "thallama_softmax": (None, [FP, I]),
             "thallama_requests_read": (VP, [S, I, I]),
+            "thallama_requests_set_sampling": (None, [VP, C.c_float, C.c_float]),
             "thallama_requests_free": (None, [VP]),
             "thallama_requests_count": (I, [VP]),
             "thallama_requests_prompt": (S, [VP, I]),
@@ -122,6 +123,10 @@ class Requests:
 
     def __len__(self):
         return lib().thallama_requests_count(self.h)
+
+    def set_sampling(self, temperature, topp=0.9):
+        """temperature 0 = greedy; default is the reference's 1.0 / 0.9."""
+        lib().thallama_requests_set_sampling(self.h, temperature, topp)
 
     def prompt(self, i):
         return lib().thallama_requests_prompt(self.h, i)

@@ -255,9 +255,16 @@ extern "C" int thallama_sample(thallama_sampler* s, float* logits) {
 // ------------------------------------------------------------------------------ request files
 struct thallama_requests {
   int max_token_len = 0, max_seq_len = 0;
+  float temperature = 1.0f, topp = 0.9f;  // the reference's per-request sampler (src/llama.cpp:897-900)
   std::vector<std::string> prompts, outputs;
   size_t cap() const { return (size_t)max_token_len * (size_t)max_seq_len; }
 };
+
+extern "C" void thallama_requests_set_sampling(thallama_requests* r, float temperature, float topp) {
+  if (!r) return;
+  r->temperature = temperature;
+  r->topp = topp;
+}
 
 extern "C" thallama_requests* thallama_requests_read(const char* path, int max_token_len, int max_seq_len) {
   std::ifstream in(path);
@@ -305,7 +312,7 @@ extern "C" int thallama_serve_requests_prefill(thallama_requests* r, const char*
   const int n_req = (int)r->prompts.size();
   const int V = vocab_size;
   std::vector<thallama_sampler*> samplers((size_t)n_req);
-  for (int i = 0; i < n_req; ++i) samplers[i] = thallama_sampler_create(V, 1.0f, 0.9f, 314028ull);
+  for (int i = 0; i < n_req; ++i) samplers[i] = thallama_sampler_create(V, r->temperature, r->topp, 314028ull);
   std::mutex mu;
   int next_req = 0;
   std::atomic<long long> gen{0};

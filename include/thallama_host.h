@@ -56,6 +56,10 @@ void thallama_requests_free(thallama_requests* r);
 int thallama_requests_count(const thallama_requests* r);
 const char* thallama_requests_prompt(const thallama_requests* r, int i);
 const char* thallama_requests_output(const thallama_requests* r, int i);
+/* Sampling of every request (default: the reference's temperature 1.0, top-p 0.9, seed
+ * 314028 per request, src/llama.cpp:897-900).  temperature 0 = greedy (argmax), an addition
+ * for token-exact runs; the seed stays 314028. */
+void thallama_requests_set_sampling(thallama_requests* r, float temperature, float topp);
 /* write_outputfile: the count, then every generated string followed by "\n". 0 on success. */
 int thallama_requests_write(const thallama_requests* r, const char* path);
 

@@ -90,6 +90,34 @@ def test_test_mode_output_file_byte_identical(gpu, host, model, tmp_path, batch,
     assert f"Total achieved token: {gen}".encode() in r.stdout
 
 
+def test_test_mode_greedy_flag(gpu, host, model, tmp_path):
+    """-g 1 (an addition): test mode decodes greedily; every output is the CPU oracle's greedy
+    continuation of its prompt (src/seq.cpp forward, argmax with the lowest index on ties)."""
+    ref, path = model
+    inp = tmp_path / "in.txt"
+    inp.write_bytes((f"{len(PROMPTS)}\n" + "\n".join(PROMPTS) + "\n").encode())
+    out = tmp_path / "out.txt"
+    run_cli([path, "-m", "test", "-f", str(inp), "-o", str(out), "-b", "2", "-g", "1", "-z", TOK], tmp_path)
+    tok = host.Tokenizer(TOK, V)
+    want = []
+    for p in PROMPTS:
+        ids = tok.encode(p)
+        token, pos, text = ids[0], 0, b""
+        while True:
+            lg = ref.forward(token, pos)
+            nxt = ids[pos + 1] if pos < len(ids) - 1 else int(np.argmax(lg))
+            pos += 1
+            if nxt in (1, 2):
+                break
+            if tok.is_safe(token, nxt):
+                text += tok.decode(token, nxt)
+            token = nxt
+            if pos >= CFG[6]:
+                break
+        want.append(text + b"\n")
+    assert out.read_bytes() == f"{len(PROMPTS)}\n".encode() + b"".join(w + b"\n" for w in want)
+
+
 def test_generate_mode_greedy(gpu, host, model, tmp_path):
     """-t 0: greedy decoding printed to stdout, identical to the CPU oracle's greedy text."""
     ref, path = model

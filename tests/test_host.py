@@ -294,3 +294,35 @@ def test_scheduler_prefill_matches_stepping(host, tok, tmp_path, workers, batch,
     # every prompt of >= 2 tokens that fits seq_len went through the callback once
     lens = [len(tok.encode(p.encode())) for p in prompts]
     assert sorted(calls) == sorted(n - 1 for n in lens if 2 <= n and n - 1 < seq_len)
+
+
+def test_scheduler_greedy_sampling(host, tok, tmp_path):
+    """set_sampling(0): every request decodes greedily (argmax, lowest index on ties)."""
+    src = tmp_path / "in.txt"
+    prompts = ["Once upon a time", "", "A brief message:"]
+    src.write_bytes((f"{len(prompts)}\n" + "\n".join(prompts) + "\n").encode())
+    seq_len = 40
+    r = host.Requests(str(src), 27, seq_len)
+    r.set_sampling(0.0)
+
+    def step(worker, toks, pos):
+        return np.stack([_fake_logits(t, p) for t, p in zip(toks, pos)])
+    gen = r.serve(TOK, V, 2, 2, step)
+    want, want_gen = [], 0
+    for p in prompts:
+        ids = tok.encode(p.encode())
+        token, pos, text = ids[0], 0, b""
+        while True:
+            nxt = ids[pos + 1] if pos < len(ids) - 1 else int(np.argmax(_fake_logits(token, pos)))
+            pos += 1
+            if nxt in (1, 2):
+                break
+            if tok.is_safe(token, nxt):
+                text += tok.decode(token, nxt)
+            token = nxt
+            if pos >= seq_len:
+                break
+        want.append(text + b"\n")
+        want_gen += pos - 1
+    assert [r.output(i) for i in range(len(prompts))] == want
+    assert gen == want_gen
