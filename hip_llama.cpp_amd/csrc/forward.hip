@@ -124,6 +124,8 @@ struct thallama_decoder {
   int* pos_h = nullptr;
   float2* rope_d = nullptr;
   float* xn_d = nullptr;        // [<=16][dim] normed rows for the matrix-core GEMV (batch >= 2)
+  signed char* xq_d = nullptr;  // int8 batched: activations quantised once per launch [8][max(dim, hidden)]
+  float* xqs_d = nullptr;       //   and their group scales
   float* mpart_d = nullptr;     // matrix-core GEMV split-K partial tiles
   unsigned* mcnt_d = nullptr;   //   and their tickets
   float* part_d = nullptr;      // attention partials [B][H][<=16 units][hs+4]
@@ -312,6 +314,8 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   (void)hipFree(d->rope_d);
   (void)hipFree(d->xn_d);
   (void)hipFree(d->mpart_d);
+  (void)hipFree(d->xq_d);
+  (void)hipFree(d->xqs_d);
   (void)hipFree(d->mcnt_d);
   (void)hipFree(d->part_d);
   (void)hipFree(d->cnt_d);
@@ -361,6 +365,8 @@ static hipError_t gemv(thallama_decoder* d, int mode, tl::GemvParams& p, const Q
   p.Q2 = t2 ? t2->q : nullptr;
   p.S2 = t2 ? t2->s : nullptr;
   p.gs = d->w8.group_size;
+  p.xq = d->xq_d;
+  p.xqs = d->xqs_d;
   return tl::launch_gemv_q8(mode, p, d->stream, d->nt);
 }
 #define Q8L(name) (d->q8 ? &d->w8.name[l] : nullptr)
@@ -826,6 +832,11 @@ extern "C" int thallama_decoder_create_q8(thallama_decoder** out, const Config* 
   thallama_decoder* d = *out;
   d->q8 = true;
   d->w8 = *w8;
+  if (batch >= 2) {
+    const size_t kmax = (size_t)(d->dim > d->hidden ? d->dim : d->hidden);
+    TL_TRY(hipMalloc(&d->xq_d, 8 * kmax));
+    TL_TRY(hipMalloc(&d->xqs_d, sizeof(float) * 8 * (kmax / 16 + 1)));
+  }
   // persistent step with int8 weights: re-check the shape (group size, LDS) and publish the
   // per-layer tensor addresses as a device table the kernel indexes by (tensor, layer)
   if (d->pok) {

@@ -67,6 +67,11 @@ struct GemvParams {
   // optional scratch [nb][K] for the matrix-core path (gemv_mfma.hpp): when set, the
   // RMSNorm / embedding prologue runs once per launch into it instead of once per block
   float* xn;
+  // optional int8 scratch (gemv_q8.hpp, batched): [<=8][K] codes + [<=8][K/gs] scales; when
+  // set, the activations are quantised once per launch (gemv_q8_prequant_kernel) instead of
+  // once per block
+  signed char* xq;
+  float* xqs;
   // optional split-K scratch for the matrix-core path: per-block partial tiles
   // [tiles][splits][2][256] and one ticket per tile (zero between launches)
   float* mpart;

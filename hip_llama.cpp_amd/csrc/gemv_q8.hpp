@@ -75,6 +75,79 @@ TL_DEVICE void stage_x_q8(const GemvParams& p, int8_t* xq, float* xsc, int kc, i
   }
 }
 
+// Batched launches: quantise every live sequence's activations ONCE (RMSNorm / embedding
+// fused as in stage_x_q8) into p.xq / p.xqs, instead of once per block (at 8 sequences the
+// per-block prologue read 8 x K activations for every 16-32 weight rows).  One block per
+// sequence; same arithmetic as stage_x_q8 (runq.c:145-171).
+template <int LPG>
+__global__ void __launch_bounds__(256) gemv_q8_prequant_kernel(GemvParams p) {
+  typedef int i4 __attribute__((ext_vector_type(4)));
+  __shared__ float red[16];
+  const int b = blockIdx.x;
+  const int K = p.K, n16 = K >> 4, ng = K / (LPG * 16);
+  const float* src = p.tok ? p.emb + (long long)p.tok[b] * K : p.x + b * p.x_stride;
+  float s = 1.f;
+  if (p.rms_w) {
+    float sq = 0.f;
+    for (int j = threadIdx.x; j < (K >> 2); j += blockDim.x) {
+      const f4 v = reinterpret_cast<const f4*>(src)[j];
+      sq = fmaf(v.x, v.x, sq); sq = fmaf(v.y, v.y, sq); sq = fmaf(v.z, v.z, sq); sq = fmaf(v.w, v.w, sq);
+    }
+    const float t = block_sum(sq, red);
+    s = __fdiv_rn(1.0f, sqrtf(__fadd_rn(__fdiv_rn(t, (float)K), 1e-5f)));
+  }
+  if (p.tok)
+    for (int j = threadIdx.x; j < (K >> 2); j += blockDim.x)
+      reinterpret_cast<f4*>(p.x_out + b * p.x_stride)[j] = reinterpret_cast<const f4*>(src)[j];
+  // 256 threads = 64 quads... of LPG threads per group; every thread one 16-value slice
+  for (int sl0 = 0; sl0 < n16; sl0 += blockDim.x) {
+    const int sl = sl0 + threadIdx.x;
+    const bool live = sl < n16;
+    f4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      v[u] = live ? reinterpret_cast<const f4*>(src + sl * 16)[u] : f4{0.f, 0.f, 0.f, 0.f};
+      if (live && p.rms_w) v[u] = rms_apply(v[u], reinterpret_cast<const f4*>(p.rms_w + sl * 16)[u], s);
+    }
+    float m = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+#pragma unroll
+    for (int o = LPG / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    const float scale = __fdiv_rn(m, 127.0f);
+    if (live) {
+      i4 packed;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q0 = q8_round(__fdiv_rn(v[u].x, scale)), q1 = q8_round(__fdiv_rn(v[u].y, scale));
+        const int q2 = q8_round(__fdiv_rn(v[u].z, scale)), q3 = q8_round(__fdiv_rn(v[u].w, scale));
+        packed[u] = (q0 & 0xFF) | ((q1 & 0xFF) << 8) | ((q2 & 0xFF) << 16) | ((q3 & 0xFF) << 24);
+      }
+      *reinterpret_cast<i4*>(p.xq + (long long)b * K + sl * 16) = packed;
+      if ((sl % LPG) == 0) p.xqs[(long long)b * ng + sl / LPG] = scale;
+    }
+  }
+}
+
+// Copy pre-quantised activations [kc, kc+kcn) of every live sequence into the LDS layout
+// stage_x_q8 produces.
+template <int NB, int LPG>
+TL_DEVICE void stage_x_q8_pre(const GemvParams& p, int8_t* xq, float* xsc, int kc, int kcn) {
+  typedef int i4 __attribute__((ext_vector_type(4)));
+  const int n16 = kcn >> 4, gsz = LPG * 16, ngc = kcn / gsz, ng = p.K / gsz;
+  for (int e = threadIdx.x; e < NB * n16; e += blockDim.x) {
+    const int b = e / n16, sl = e % n16;
+    i4 v = i4{0, 0, 0, 0};
+    if (b < p.nb) v = *reinterpret_cast<const i4*>(p.xq + (long long)b * p.K + kc + sl * 16);
+    *reinterpret_cast<i4*>(xq + b * kcn + sl * 16) = v;
+  }
+  for (int e = threadIdx.x; e < NB * ngc; e += blockDim.x) {
+    const int b = e / ngc, gi = e % ngc;
+    xsc[b * ngc + gi] = b < p.nb ? p.xqs[(long long)b * ng + kc / gsz + gi] : 0.f;
+  }
+}
+
 template <int MODE>
 TL_DEVICE void q8_item_row(const GemvParams& p, int item, int r, const int8_t*& q, const float*& s) {
   const long long K = p.K, ng = p.K / p.gs;
@@ -159,7 +232,8 @@ __global__ void __launch_bounds__(WAVES * 64) gemv_q8_kernel(GemvParams p, int k
   for (int kc = 0; kc < p.K; kc += kc_max) {
     const int kcn = min(kc_max, p.K - kc);
     if (kc) __syncthreads();
-    stage_x_q8<NB, LPG>(p, xq, xsc, kc, kcn, ss);
+    if (p.xq) stage_x_q8_pre<NB, LPG>(p, xq, xsc, kc, kcn);
+    else stage_x_q8<NB, LPG>(p, xq, xsc, kc, kcn, ss);
     __syncthreads();
     const int nfull = kcn >> 10;
     int j = 0;

@@ -124,6 +124,18 @@ static hipError_t launch_q8_mode(const GemvParams& p0, hipStream_t s, bool nt) {
       if (p.kc) p.kc += (long long)b0 * p.kv_b_stride;
       if (p.vc) p.vc += (long long)b0 * p.kv_b_stride;
     }
+    if (p.nb >= 2 && p.xq && p.xqs) {
+      // quantise once per launch, then the GEMV copies the codes (no per-block prologue)
+      const int lpg = p.gs / 16;
+      if (lpg == 2) hipLaunchKernelGGL(gemv_q8_prequant_kernel<2>, dim3(p.nb), dim3(256), 0, s, p);
+      else if (lpg == 4) hipLaunchKernelGGL(gemv_q8_prequant_kernel<4>, dim3(p.nb), dim3(256), 0, s, p);
+      else hipLaunchKernelGGL(gemv_q8_prequant_kernel<8>, dim3(p.nb), dim3(256), 0, s, p);
+      p.rms_w = nullptr;
+      p.tok = nullptr;
+      p.x_out = nullptr;
+    } else {
+      p.xq = nullptr;
+    }
     if (p.nb == 1) launch_q8_nb<MODE, 1>(p, s, nt);
     else if (p.nb == 2) launch_q8_nb<MODE, 2>(p, s, nt);
     else if (p.nb <= 4) launch_q8_nb<MODE, 4>(p, s, nt);

@@ -26,7 +26,7 @@ def build(tl, oracle, cfg, seed, batch=1):
 
 
 @pytest.mark.parametrize("cfg", CFGS)
-@pytest.mark.parametrize("n", [1, 7, 64, 130])
+@pytest.mark.parametrize("n", [1, 7, 20, 64, 81, 130])
 def test_prefill_then_decode_matches_oracle(gpu, oracle, cfg, n):
     model, state, dec, ref = build(gpu, oracle, cfg, 31)
     toks = np.random.default_rng(n).integers(0, cfg[5], n + 1).tolist()
