@@ -313,20 +313,38 @@ TL_DEVICE void consume_any(const PGeo& g, int slot, int lane, const f4 (&buf)[PL
   else consume_slot(g, slot, lane, buf, xs, res);
 }
 
+// Slot indices past the first two per wave are dealt dynamically from a block-wide LDS
+// counter (reset by the control wave between phases): the waves of a block stream at
+// different rates (measured: the slowest wave of a block finished its static round-robin
+// share up to ~25% after the fastest), and a phase ends with its slowest wave.  Slots a wave
+// holds only ever increase (A's next slot is taken after B's), so the first invalid slot
+// in A ends the wave's phase; every refill is still exactly one slot of loads (past the end:
+// zero-size), so the compiler's in-order vmcnt bookkeeping stays exact.
+TL_DEVICE int take_slot(unsigned* ctr, int lane) {
+  unsigned v = 0;
+  if (lane == 0) v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return 2 * NSW + (int)__builtin_amdgcn_readlane(v, 0);
+}
+
 template <bool Q8>
 TL_DEVICE void run_gemv(const PDesc& d, const PGeo& g, const PStep& p, int sw, int lane, const f4* xs,
                         const signed char* xq, const float* xsc, float* res, f4 (&A)[PL], f4 (&B)[PL],
-                        float (&SA)[PL], float (&SB)[PL]) {
-  const int nk = g.nslot > sw ? (g.nslot - sw + NSW - 1) / NSW : 0;
+                        float (&SA)[PL], float (&SB)[PL], unsigned* ctr, unsigned long long* ts) {
+  int sa = sw, sb = sw + NSW;  // the slots A and B hold (the phase's prefetch)
+  bool first = true;
   // sched_barrier: keep each refill behind the slot's last use (no third register set)
-  for (int k = 0; k < nk; k += 2) {
-    consume_any<Q8>(g, sw + k * NSW, lane, A, SA, xs, xq, xsc, res);
+  while (sa < g.nslot) {
+    consume_any<Q8>(g, sa, lane, A, SA, xs, xq, xsc, res);
+    if (ts && first && lane == 0) *ts = __builtin_amdgcn_s_memrealtime();  // first slot landed
+    first = false;
     __builtin_amdgcn_sched_barrier(0);
-    load_any<Q8>(d, g, p, sw + (k + 2) * NSW, lane, A, SA);
+    sa = take_slot(ctr, lane);
+    load_any<Q8>(d, g, p, sa, lane, A, SA);
     __builtin_amdgcn_sched_barrier(0);
-    if (k + 1 < nk) consume_any<Q8>(g, sw + (k + 1) * NSW, lane, B, SB, xs, xq, xsc, res);
+    if (sb < g.nslot) consume_any<Q8>(g, sb, lane, B, SB, xs, xq, xsc, res);
     __builtin_amdgcn_sched_barrier(0);
-    load_any<Q8>(d, g, p, sw + (k + 3) * NSW, lane, B, SB);
+    sb = take_slot(ctr, lane);
+    load_any<Q8>(d, g, p, sb, lane, B, SB);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -512,12 +530,14 @@ TL_DEVICE void grid_barrier(const PStep& p) {
   __syncthreads();
 }
 
-// Optional timeline (PStep::trace): the control wave of every block stamps the 100-MHz
-// real-time clock at phase start, input staged, all slots reduced, epilogue issued.
+// Optional timeline (PStep::trace, [grid][phase][8]): the control wave of every block stamps
+// the 100-MHz real-time clock at phase start, input staged, all slots reduced, epilogue
+// issued (0-3); streaming wave 0 at input staged, first slot consumed, last slot consumed,
+// next phase's slots issued (4-7).
 #define TRACE(k)                                                                                \
   do {                                                                                          \
     if (p.trace && lane == 0)                                                                   \
-      p.trace[((long long)blockIdx.x * nph + ph) * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+      p.trace[((long long)blockIdx.x * nph + ph) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 // The phase sequence as seen by one wave.  ROLE0 = the control wave (epilogues, attention,
@@ -527,12 +547,14 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
                       float* rmsw, f4* xs, signed char* xq, float* xsc, unsigned tb) {
   const int G = gridDim.x;
   const int nph = 5 * p.L + 1;
+  unsigned* ctr = reinterpret_cast<unsigned*>(red + 15);  // dynamic slot counter (red[0..PW) is the norm sum)
   if constexpr (ROLE0) {
     // this block's slice of the residual stream starts as the token's embedding row
     const PGeo gx = geo<Q8>(make_desc<Q8>(p, PK_WO, 0, tb));
     const float* er = p.emb + (long long)p.tok[0] * p.dim + gx.i0;
     for (int it = lane; it < gx.ni; it += 64) xres[it] = er[it];
     preload_rms(p.L > 0 ? p.rms_att : p.rms_final, p.dim, rmsw, lane);
+    if (lane == 0) *ctr = 0u;
     __syncthreads();  // first norm weights preloaded
     for (int ph = 0; ph < nph; ++ph) {
       const int l = ph / 5;
@@ -562,6 +584,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
       if (kind == PK_QKV) preload_rms(p.rms_ffn + (long long)l * p.dim, p.dim, rmsw, lane);
       if (kind == PK_UP) preload_rms(l + 1 < p.L ? p.rms_att + (long long)(l + 1) * p.dim : p.rms_final, p.dim, rmsw, lane);
       __syncthreads();  // every slot reduced into res
+      if (lane == 0) *ctr = 0u;  // next GEMV phase's slot counter (used after its staging barrier)
       TRACE(2);
       epilogue(d, g, p, res, xres, lane, l);
       TRACE(3);
@@ -584,13 +607,18 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
       const PDesc d = make_desc<Q8>(p, kind, kind == PK_CLS ? p.L : l, tb);
       const PGeo g = geo<Q8>(d);
       stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, wave, lane);
-      run_gemv<Q8>(d, g, p, sw, lane, xs, xq, xsc, res, A, B, SA, SB);
+      const bool tr = p.trace && sw == 0;
+      if (tr) TRACE(4);
+      run_gemv<Q8>(d, g, p, sw, lane, xs, xq, xsc, res, A, B, SA, SB, ctr,
+                   tr ? p.trace + ((long long)blockIdx.x * nph + ph) * 8 + 5 : nullptr);
+      if (tr) TRACE(6);
       if (kind != PK_CLS) {
         const PDesc nd = next_desc<Q8>(p, kind, l, tb);
         const PGeo ng = geo<Q8>(nd);
         load_any<Q8>(nd, ng, p, sw, lane, A, SA);
         load_any<Q8>(nd, ng, p, sw + NSW, lane, B, SB);
       }
+      if (tr) TRACE(7);
       __syncthreads();  // every slot reduced into res
     }
   }

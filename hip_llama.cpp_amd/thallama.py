@@ -400,7 +400,7 @@ class Decoder:
 
     def ptrace(self, enable=True):
         """Enable the persistent-step timeline; returns the stamps of the last launch as a
-        [grid, phases, 4] uint64 array (100-MHz clock) once a launch has run."""
+        [grid, phases, 8] uint64 array (100-MHz clock) once a launch has run."""
         n = lib().thallama_decoder_ptrace(self.h, int(enable), None, 0)
         check(0 if n >= 0 else n, "decoder_ptrace")
         out = np.zeros(n, np.uint64)

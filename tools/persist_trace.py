@@ -46,8 +46,8 @@ def main():
     t = dec.ptrace(False).astype(np.int64)
     L = cfg[2]
     nph = 5 * L + 1
-    G = t.size // (nph * 4)
-    t = t.reshape(G, nph, 4)
+    G = t.size // (nph * 8)
+    t = t.reshape(G, nph, 8)
     t = (t - t[:, 0, 0].min()) * 0.01  # us
     dim, hid, kvd, V = cfg[0], cfg[1], cfg[0] * cfg[4] // cfg[3], cfg[5]
     esz = 4 if args.dtype == "f32" else 1 + 4 / 64  # int8 + one fp32 scale per 64
@@ -85,6 +85,16 @@ def main():
         print(f"{kind:9s} stream per block: min {st.min():.2f} med {np.median(st):.2f} max {st.max():.2f}; "
               f"by blockIdx%8: " + " ".join(f"{v:.1f}" for v in byx))
         out[kind + "_stream_by_xcd"] = byx
+    # streaming wave 0 of every block: staged -> first slot consumed (waiting for data that was
+    # prefetched during the hand-off), first -> last slot, issue of the next phase's slots
+    print(f"{'kind':9s}{'first':>8s}{'rest':>8s}{'issue':>8s}   (streaming wave 0, medians over blocks, us)")
+    for kind, k in (("qkv", 0), ("wo", 2), ("ffn_up", 3), ("ffn_down", 4)):
+        phs = list(range(k, nph - 1, 5))
+        f = np.median([t[:, ph, 5] - t[:, ph, 4] for ph in phs])
+        r = np.median([t[:, ph, 6] - t[:, ph, 5] for ph in phs])
+        i = np.median([t[:, ph, 7] - t[:, ph, 6] for ph in phs])
+        print(f"{kind:9s}{f:8.2f}{r:8.2f}{i:8.2f}")
+        out[kind + "_stream_wave"] = {"first": float(f), "rest": float(r), "issue": float(i)}
     if args.json:
         with open(args.json, "w") as f:
             json.dump(out, f, indent=1)
