@@ -605,10 +605,10 @@ static int check_persist(thallama_decoder* d) {
 extern "C" int thallama_decoder_persistent(thallama_decoder* d) { return d && use_persist(d) ? 1 : 0; }
 
 // Timeline of the persistent step (tools/persist_trace.py): enable allocates the buffer;
-// every later launch overwrites it; copy returns [grid][5L+1][8] 100-MHz stamps.
+// every later launch overwrites it; copy returns [grid][5L+1][kTraceSlots] 100-MHz stamps.
 extern "C" int thallama_decoder_ptrace(thallama_decoder* d, int enable, unsigned long long* host, size_t n) {
   if (!d) return (int)hipErrorInvalidValue;
-  const size_t need = (size_t)d->ncu * (5 * d->L + 1) * 8;
+  const size_t need = (size_t)d->ncu * (5 * d->L + 1) * tl::kTraceSlots;
   if (enable && !d->ptrace) {
     TL_TRY(hipMalloc(&d->ptrace, need * sizeof(unsigned long long)));
     TL_TRY(hipMemset(d->ptrace, 0, need * sizeof(unsigned long long)));

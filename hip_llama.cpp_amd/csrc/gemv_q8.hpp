@@ -30,6 +30,40 @@ TL_DEVICE int q8_round(float v) {
   return r != r ? 0 : (int)r;
 }
 
+typedef int q8i4 __attribute__((ext_vector_type(4)));
+
+// 16 activations (one thread's slice of a group) -> 16 int8 codes packed in a q8i4:
+// q = round(x / scale), runq.c:167, bit-identical to the IEEE division.  The division costs
+// ~10 VALU instructions and every block of the persistent step quantises the whole vector,
+// so one correctly rounded reciprocal r = RN(1/scale) per thread and, per value,
+// y = RN(x r), the exact remainder e = x - y scale (FMA) and RN(y + r e), which is RN(x / scale)
+// (Markstein's theorem; checked against the division on 1.28e9 values, tools/probes/q8div.c).
+// Scales outside [1e-30, 1e30] (an all-zero group: scale 0 -> NaN -> 0) divide.
+TL_DEVICE bool q8_fast_scale(float scale) { return scale >= 1e-30f && scale <= 1e30f; }
+TL_DEVICE float q8_div_fast(float x, float scale, float r) {
+  const float y = __fmul_rn(x, r);
+  return __builtin_fmaf(__builtin_fmaf(-y, scale, x), r, y);
+}
+TL_DEVICE q8i4 q8_pack16(const f4 (&v)[4], float scale) {
+  float q[16];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) { q[4 * u] = v[u].x; q[4 * u + 1] = v[u].y; q[4 * u + 2] = v[u].z; q[4 * u + 3] = v[u].w; }
+  if (q8_fast_scale(scale)) {
+    const float r = __fdiv_rn(1.0f, scale);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) q[i] = q8_div_fast(q[i], scale, r);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) q[i] = __fdiv_rn(q[i], scale);
+  }
+  q8i4 packed;
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    packed[u] = (q8_round(q[4 * u]) & 0xFF) | ((q8_round(q[4 * u + 1]) & 0xFF) << 8) |
+                ((q8_round(q[4 * u + 2]) & 0xFF) << 16) | ((q8_round(q[4 * u + 3]) & 0xFF) << 24);
+  return packed;
+}
+
 TL_DEVICE f4 rms_apply(f4 v, f4 w, float s) {
   return f4{__fmul_rn(w.x, __fmul_rn(s, v.x)), __fmul_rn(w.y, __fmul_rn(s, v.y)), __fmul_rn(w.z, __fmul_rn(s, v.z)),
             __fmul_rn(w.w, __fmul_rn(s, v.w))};
@@ -39,7 +73,6 @@ TL_DEVICE f4 rms_apply(f4 v, f4 w, float s) {
 // xsc [NB][kcn/gs]; TPG = gs/16 threads per group, 16 values per thread.
 template <int NB, int TPG>
 TL_DEVICE void stage_x_q8(const GemvParams& p, int8_t* xq, float* xsc, int kc, int kcn, const float* ss) {
-  typedef int i4 __attribute__((ext_vector_type(4)));
   const int n16 = kcn >> 4;  // 16-value slices per sequence
   for (int e = threadIdx.x; e < NB * n16; e += blockDim.x) {
     const int b = e / n16, sl = e % n16;  // TPG consecutive threads own one group
@@ -63,14 +96,7 @@ TL_DEVICE void stage_x_q8(const GemvParams& p, int8_t* xq, float* xsc, int kc, i
 #pragma unroll
     for (int o = TPG / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
     const float scale = __fdiv_rn(m, 127.0f);
-    i4 packed;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int q0 = q8_round(__fdiv_rn(v[u].x, scale)), q1 = q8_round(__fdiv_rn(v[u].y, scale));
-      const int q2 = q8_round(__fdiv_rn(v[u].z, scale)), q3 = q8_round(__fdiv_rn(v[u].w, scale));
-      packed[u] = (q0 & 0xFF) | ((q1 & 0xFF) << 8) | ((q2 & 0xFF) << 16) | ((q3 & 0xFF) << 24);
-    }
-    *reinterpret_cast<i4*>(xq + b * kcn + sl * 16) = packed;
+    *reinterpret_cast<q8i4*>(xq + b * kcn + sl * 16) = q8_pack16(v, scale);
     if ((sl % TPG) == 0) xsc[b * (kcn / (TPG * 16)) + sl / TPG] = scale;
   }
 }
@@ -81,7 +107,6 @@ TL_DEVICE void stage_x_q8(const GemvParams& p, int8_t* xq, float* xsc, int kc, i
 // sequence; same arithmetic as stage_x_q8 (runq.c:145-171).
 template <int LPG>
 __global__ void __launch_bounds__(256) gemv_q8_prequant_kernel(GemvParams p) {
-  typedef int i4 __attribute__((ext_vector_type(4)));
   __shared__ float red[16];
   const int b = blockIdx.x;
   const int K = p.K, n16 = K >> 4, ng = K / (LPG * 16);
@@ -117,14 +142,7 @@ __global__ void __launch_bounds__(256) gemv_q8_prequant_kernel(GemvParams p) {
     for (int o = LPG / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
     const float scale = __fdiv_rn(m, 127.0f);
     if (live) {
-      i4 packed;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int q0 = q8_round(__fdiv_rn(v[u].x, scale)), q1 = q8_round(__fdiv_rn(v[u].y, scale));
-        const int q2 = q8_round(__fdiv_rn(v[u].z, scale)), q3 = q8_round(__fdiv_rn(v[u].w, scale));
-        packed[u] = (q0 & 0xFF) | ((q1 & 0xFF) << 8) | ((q2 & 0xFF) << 16) | ((q3 & 0xFF) << 24);
-      }
-      *reinterpret_cast<i4*>(p.xq + (long long)b * K + sl * 16) = packed;
+      *reinterpret_cast<q8i4*>(p.xq + (long long)b * K + sl * 16) = q8_pack16(v, scale);
       if ((sl % LPG) == 0) p.xqs[(long long)b * ng + sl / LPG] = scale;
     }
   }
@@ -171,7 +189,6 @@ TL_DEVICE void q8_item_row(const GemvParams& p, int item, int r, const int8_t*& 
   s = S + row * ng;
 }
 
-typedef int q8i4 __attribute__((ext_vector_type(4)));
 
 // One wave-load (16 int8 per lane) of one row against every sequence's activations.
 template <int NB, int LPG>

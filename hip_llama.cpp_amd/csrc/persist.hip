@@ -45,6 +45,11 @@ constexpr int NSW = PW - 1;  // streaming waves per block
 constexpr int SB = 4;        // staged float4 per thread and batch (granule loads in flight)
 constexpr int kPResidFloats = 256;  // residual-stream slice per block (LDS)
 constexpr unsigned kSpinLimit = 1u << 18;
+#ifndef PERSIST_XCD_SKEW
+#define PERSIST_XCD_SKEW 4
+#endif
+constexpr unsigned kXcdSkew = PERSIST_XCD_SKEW;  // percent (geo)
+#define TL_HOST_DEVICE_INLINE __host__ __device__ inline
 
 enum PKind : int { PK_QKV = 0, PK_ATTN = 1, PK_WO = 2, PK_UP = 3, PK_DOWN = 4, PK_CLS = 5 };
 
@@ -143,14 +148,22 @@ struct PGeo {
   int nslot; // slots of this block
 };
 
+// Cumulative partition weight of blocks [0, b) (see geo).
+TL_HOST_DEVICE_INLINE unsigned part_weight(unsigned b) { return (b >> 1) * 200u + (b & 1u) * (100u + kXcdSkew); }
+
 template <bool Q8>
 TL_DEVICE PGeo geo(const PDesc& d) {
   PGeo g;
   g.rowb = Q8 ? d.K : d.K * 4;
   g.nch = Q8 ? (d.K + 4095) / 4096 : (d.K + PL * 256 - 1) / (PL * 256);
-  const long long G = gridDim.x, bi = blockIdx.x;
-  g.i0 = (int)(bi * d.n_items / G);
-  g.ni = (int)((bi + 1) * d.n_items / G) - g.i0;
+  // Blocks with odd blockIdx (XCDs 1, 3, 5, 7 under round-robin dispatch) stream measurably
+  // slower, so the items are dealt in proportion to 100 + kXcdSkew (even) and
+  // 100 - kXcdSkew (odd); speed only, any placement is correct.  32-bit: n_items * 200 *
+  // gridDim / 2 < 2^32 for every supported shape (persistent_prepare).
+  const unsigned G = gridDim.x, bi = blockIdx.x, n = (unsigned)d.n_items;
+  const unsigned wt = part_weight(G);
+  g.i0 = (int)(n * part_weight(bi) / wt);
+  g.ni = (int)(n * part_weight(bi + 1) / wt) - g.i0;
   g.nres = g.ni * d.rpi * g.nch;
   g.nslot = Q8 ? (g.nres + 1) / 2 : g.nres;
   return g;
@@ -170,9 +183,8 @@ TL_DEVICE const float* row_ptr(const PDesc& d, const PStep& p, int R) {
 }
 
 // Issue the 8 wave-loads of `slot` into buf: raw buffer loads over one row (the resource's
-// size is what is left of the row, so loads past its end return 0 without touching memory,
-// and a slot past the block's end is a zero-size resource: every slot is exactly PL loads
-// and the compiler's vmcnt bookkeeping stays exact — A/B double buffer, vmcnt(PL)).
+// size is what is left of the row, so loads past its end return 0 without touching memory;
+// a slot past the block's end gives a zero-size resource, but callers skip those).
 TL_DEVICE void load_slot(const PDesc& d, const PGeo& g, const PStep& p, int slot, int lane, f4 (&buf)[PL]) {
   const bool sv = slot < g.nslot;
   const int rl = slot / g.nch, c = slot - rl * g.nch;
@@ -254,22 +266,16 @@ TL_DEVICE void load_slot_q8(const PDesc& d, const PGeo& g, const PStep& p, int s
     const auto ss = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(srow) + (off >> 6), (short)0,
                                                       sleft > 0 ? sleft : 0, 0x00020000);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 4; ++u)
       buf[h * 4 + u] =
           __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16 + u * 1024, 0, 2 /*nt*/));
-      sc[h * 4 + u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ss, ((u * 1024 + lane * 16) >> 6) * 4, 0, 0));
-    }
+    // one scale per lane: lane 4q + j holds group j*16 + q of the chunk, the group whose int32
+    // sum the quad reduce-scatter in consume_slot_q8 leaves in that lane
+    sc[h] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ss, ((lane & 3) * 16 + (lane >> 2)) * 4, 0, 0));
   }
 }
 
-// Sum over a quad of lanes (the 4 lanes of one 64-wide group), exact in int32.
-TL_DEVICE int quad_sum(int v) {
-  v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-  v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-  return v;
-}
-
-// runq.c:317-342 per chunk: per group the int32 dot (v_dot4_i32_i8 + quad sum), then
+// runq.c:317-342 per chunk: per group the int32 dot (v_dot4_i32_i8 + quad reduce-scatter), then
 // val += ((float)ival * w.s) * x.s; chunk sums land in res in chunk order.
 TL_DEVICE void consume_slot_q8(const PGeo& g, int slot, int lane, const f4 (&buf)[PL], const float (&sc)[PL],
                                const signed char* xq, const float* xsc, float* res) {
@@ -278,18 +284,27 @@ TL_DEVICE void consume_slot_q8(const PGeo& g, int slot, int lane, const f4 (&buf
     const int Q = 2 * slot + h;
     const int c = Q % g.nch;
     float a = 0.f;
+    int dd[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int kb = c * 4096 + u * 1024 + lane * 16;
       const q8i4 xv = *reinterpret_cast<const q8i4*>(xq + kb);
       const q8i4 wv = __builtin_bit_cast(q8i4, buf[h * 4 + u]);
-      int dd = __builtin_amdgcn_sdot4(wv.x, xv.x, 0, false);
-      dd = __builtin_amdgcn_sdot4(wv.y, xv.y, dd, false);
-      dd = __builtin_amdgcn_sdot4(wv.z, xv.z, dd, false);
-      dd = __builtin_amdgcn_sdot4(wv.w, xv.w, dd, false);
-      dd = quad_sum(dd);
-      if ((lane & 3) == 0) a += __fmul_rn(__fmul_rn((float)dd, sc[h * 4 + u]), xsc[kb >> 6]);
+      int t = __builtin_amdgcn_sdot4(wv.x, xv.x, 0, false);
+      t = __builtin_amdgcn_sdot4(wv.y, xv.y, t, false);
+      t = __builtin_amdgcn_sdot4(wv.z, xv.z, t, false);
+      dd[u] = __builtin_amdgcn_sdot4(wv.w, xv.w, t, false);
     }
+    // quad reduce-scatter (exact int32): lane 4q + j ends with the quad's sum for u = j, i.e.
+    // group j*16 + q of the chunk (3 DPP moves instead of a full quad sum per u)
+    const bool b0 = lane & 1, b1 = lane & 2;
+    int s0 = b0 ? dd[1] : dd[0], s1 = b0 ? dd[3] : dd[2];
+    s0 += __builtin_amdgcn_mov_dpp(b0 ? dd[0] : dd[1], 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    s1 += __builtin_amdgcn_mov_dpp(b0 ? dd[2] : dd[3], 0xB1, 0xF, 0xF, false);
+    int gs = b1 ? s1 : s0;
+    gs += __builtin_amdgcn_mov_dpp(b1 ? s0 : s1, 0x4E, 0xF, 0xF, false);       // quad_perm [2,3,0,1]
+    const int grp = c * 64 + (lane & 3) * 16 + (lane >> 2);
+    a = __fmul_rn(__fmul_rn((float)gs, sc[h]), xsc[grp]);  // runq.c:334
     a = wave_sum(a);
     if (lane == 0 && Q < g.nres) res[Q] = a;
     __builtin_amdgcn_sched_barrier(0);
@@ -318,8 +333,9 @@ TL_DEVICE void consume_any(const PGeo& g, int slot, int lane, const f4 (&buf)[PL
 // different rates (measured: the slowest wave of a block finished its static round-robin
 // share up to ~25% after the fastest), and a phase ends with its slowest wave.  Slots a wave
 // holds only ever increase (A's next slot is taken after B's), so the first invalid slot
-// in A ends the wave's phase; every refill is still exactly one slot of loads (past the end:
-// zero-size), so the compiler's in-order vmcnt bookkeeping stays exact.
+// in A ends the wave's phase.  Refills past the phase's end are skipped rather than issued
+// as zero-size loads: at the phase end those issues sat on the path to the epilogue (+6-8%
+// int8), and the compiler's vmcnt bookkeeping stays tight enough over the two branches.
 TL_DEVICE int take_slot(unsigned* ctr, int lane) {
   unsigned v = 0;
   if (lane == 0) v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -339,13 +355,42 @@ TL_DEVICE void run_gemv(const PDesc& d, const PGeo& g, const PStep& p, int sw, i
     first = false;
     __builtin_amdgcn_sched_barrier(0);
     sa = take_slot(ctr, lane);
-    load_any<Q8>(d, g, p, sa, lane, A, SA);
+    if (sa < g.nslot) load_any<Q8>(d, g, p, sa, lane, A, SA);
     __builtin_amdgcn_sched_barrier(0);
     if (sb < g.nslot) consume_any<Q8>(g, sb, lane, B, SB, xs, xq, xsc, res);
     __builtin_amdgcn_sched_barrier(0);
     sb = take_slot(ctr, lane);
-    load_any<Q8>(d, g, p, sb, lane, B, SB);
+    if (sb < g.nslot) load_any<Q8>(d, g, p, sb, lane, B, SB);
     __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Granule sweep of the phase input into the LDS strip by threads t, t + T, ...: batches of NB
+// float4 (2*NB loads in flight per thread), then re-poll what was late.  sq: sum of squares.
+template <int NB>
+TL_DEVICE void gather(__amdgpu_buffer_rsrc_t r, unsigned tag, int n4, int pad4, int t, int T, f4* xs, float& sq,
+                      unsigned* err) {
+  for (int k0 = 0; k0 * T < pad4; k0 += NB) {
+    v4u a[NB], b[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int j = t + (k0 + k) * T;
+      if (j < n4) {
+        a[k] = ld16_sc1(r, (unsigned)j * 32u);
+        b[k] = ld16_sc1(r, (unsigned)j * 32u + 16u);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int j = t + (k0 + k) * T;
+      if (j < pad4) {
+        f4 v = f4{0.f, 0.f, 0.f, 0.f};
+        if (j < n4)
+          v = gran4_ok(a[k], b[k], tag) ? gran4_val(a[k], b[k]) : gran_wait4(r, (unsigned)j * 32u, tag, err);
+        sq = fmaf(v.x, v.x, sq); sq = fmaf(v.y, v.y, sq); sq = fmaf(v.z, v.z, sq); sq = fmaf(v.w, v.w, sq);
+        xs[j] = v;
+      }
+    }
   }
 }
 
@@ -356,7 +401,7 @@ TL_DEVICE void run_gemv(const PDesc& d, const PGeo& g, const PStep& p, int sw, i
 // the token's embedding row (weights: plain loads).  Ends with a workgroup barrier.
 template <bool Q8>
 TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, signed char* xq, float* xsc,
-                     const float* rmsw, float* red, int wave, int lane) {
+                     const float* rmsw, float* red, int wave, int lane, unsigned long long* ts) {
   const int n4 = d.K >> 2, pad4 = Q8 ? n4 : g.nch * PL * 64;
   float sq = 0.f;
   if (!d.gin) {
@@ -367,32 +412,11 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, sign
       xs[j] = v;
     }
   } else {
-    const auto r = rsrc_of(d.gin);
-    // batches of SB float4 (2*SB loads in flight per thread), then re-poll what was late
-    for (int k0 = 0; k0 * PT < pad4; k0 += SB) {
-      v4u a[SB], b[SB];
-#pragma unroll
-      for (int k = 0; k < SB; ++k) {
-        const int j = threadIdx.x + (k0 + k) * PT;
-        if (j < n4) {
-          a[k] = ld16_sc1(r, (unsigned)j * 32u);
-          b[k] = ld16_sc1(r, (unsigned)j * 32u + 16u);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < SB; ++k) {
-        const int j = threadIdx.x + (k0 + k) * PT;
-        if (j < pad4) {
-          f4 v = f4{0.f, 0.f, 0.f, 0.f};
-          if (j < n4)
-            v = gran4_ok(a[k], b[k], d.tag_in) ? gran4_val(a[k], b[k])
-                                               : gran_wait4(r, (unsigned)j * 32u, d.tag_in, p.err);
-          sq = fmaf(v.x, v.x, sq); sq = fmaf(v.y, v.y, sq); sq = fmaf(v.z, v.z, sq); sq = fmaf(v.w, v.w, sq);
-          xs[j] = v;
-        }
-      }
-    }
+    // every wave sweeps (the control wave alone, 16-24 loads in flight, was 1.4x slower per
+    // step: the sweep is bound by loads in flight, not by the streaming waves' queued slots)
+    gather<SB>(rsrc_of(d.gin), d.tag_in, n4, pad4, threadIdx.x, PT, xs, sq, p.err);
   }
+  if (ts && lane == 0) ts[wave == 0 ? 8 : 10] = __builtin_amdgcn_s_memrealtime();  // input gathered
   if (d.rms) {
     // reference rmsnorm (src/seq.cpp:3-16): ss = 1/sqrtf(sum/size + 1e-5f); the block sum
     // is taken in a fixed order (waves 0..PW-1), so every block gets the same ss
@@ -411,6 +435,7 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, sign
                  __fmul_rn(w.z, __fmul_rn(s, v.z)), __fmul_rn(w.w, __fmul_rn(s, v.w))};
     }
   }
+  if (ts && lane == 0 && wave == 0) ts[9] = __builtin_amdgcn_s_memrealtime();  // normalised
   if constexpr (Q8) {
     // runq.c:145-171 quantize over the padded strip: 4 consecutive threads (one quad) per
     // group of 64, 16 values each; scale = max|x| / 127, q = round(x / scale)
@@ -427,14 +452,7 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, sign
       m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0xB1, 0xF, 0xF, false)));
       m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0x4E, 0xF, 0xF, false)));
       const float scale = __fdiv_rn(m, 127.0f);
-      q8i4 packed;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int q0 = q8_round(__fdiv_rn(v[u].x, scale)), q1 = q8_round(__fdiv_rn(v[u].y, scale));
-        const int q2 = q8_round(__fdiv_rn(v[u].z, scale)), q3 = q8_round(__fdiv_rn(v[u].w, scale));
-        packed[u] = (q0 & 0xFF) | ((q1 & 0xFF) << 8) | ((q2 & 0xFF) << 16) | ((q3 & 0xFF) << 24);
-      }
-      *reinterpret_cast<q8i4*>(xq + sl * 16) = packed;
+      *reinterpret_cast<q8i4*>(xq + sl * 16) = q8_pack16(v, scale);
       if ((sl & 3) == 0) xsc[sl >> 2] = scale;
     }
   }
@@ -530,14 +548,14 @@ TL_DEVICE void grid_barrier(const PStep& p) {
   __syncthreads();
 }
 
-// Optional timeline (PStep::trace, [grid][phase][8]): the control wave of every block stamps
-// the 100-MHz real-time clock at phase start, input staged, all slots reduced, epilogue
-// issued (0-3); streaming wave 0 at input staged, first slot consumed, last slot consumed,
-// next phase's slots issued (4-7).
+// Optional timeline (PStep::trace, [grid][phase][kTraceSlots]): the control wave of every block
+// stamps the 100-MHz real-time clock at phase start, input staged, all slots reduced, epilogue
+// issued (0-3), input gathered and normalised (8-9); streaming wave 0 at input staged, first
+// slot consumed, last slot consumed, next phase's slots issued (4-7), input gathered (10).
 #define TRACE(k)                                                                                \
   do {                                                                                          \
     if (p.trace && lane == 0)                                                                   \
-      p.trace[((long long)blockIdx.x * nph + ph) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+      p.trace[((long long)blockIdx.x * nph + ph) * kTraceSlots + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 // The phase sequence as seen by one wave.  ROLE0 = the control wave (epilogues, attention,
@@ -579,7 +597,8 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
       }
       const PDesc d = make_desc<Q8>(p, kind, l, tb);
       const PGeo g = geo<Q8>(d);
-      stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, wave, lane);
+      stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, wave, lane,
+                p.trace ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots : nullptr);
       TRACE(1);
       if (kind == PK_QKV) preload_rms(p.rms_ffn + (long long)l * p.dim, p.dim, rmsw, lane);
       if (kind == PK_UP) preload_rms(l + 1 < p.L ? p.rms_att + (long long)(l + 1) * p.dim : p.rms_final, p.dim, rmsw, lane);
@@ -606,20 +625,23 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
       if (kind == PK_ATTN) continue;
       const PDesc d = make_desc<Q8>(p, kind, kind == PK_CLS ? p.L : l, tb);
       const PGeo g = geo<Q8>(d);
-      stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, wave, lane);
       const bool tr = p.trace && sw == 0;
+      stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, wave, lane,
+                tr ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots : nullptr);
       if (tr) TRACE(4);
       run_gemv<Q8>(d, g, p, sw, lane, xs, xq, xsc, res, A, B, SA, SB, ctr,
-                   tr ? p.trace + ((long long)blockIdx.x * nph + ph) * 8 + 5 : nullptr);
+                   tr ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots + 5 : nullptr);
       if (tr) TRACE(6);
+      // every slot reduced into res: the control wave's epilogue (the hand-off every other
+      // block waits for) starts now, not after this wave's next-phase issue (measured +5%)
+      __syncthreads();
       if (kind != PK_CLS) {
         const PDesc nd = next_desc<Q8>(p, kind, l, tb);
         const PGeo ng = geo<Q8>(nd);
-        load_any<Q8>(nd, ng, p, sw, lane, A, SA);
-        load_any<Q8>(nd, ng, p, sw + NSW, lane, B, SB);
+        if (sw < ng.nslot) load_any<Q8>(nd, ng, p, sw, lane, A, SA);
+        if (sw + NSW < ng.nslot) load_any<Q8>(nd, ng, p, sw + NSW, lane, B, SB);
       }
       if (tr) TRACE(7);
-      __syncthreads();  // every slot reduced into res
     }
   }
   grid_barrier(p);
@@ -686,20 +708,29 @@ bool persistent_prepare(PStep& p, int ncu, const char** why) {
   if (p.dim % 256 || p.hid % 256) return fail("dim and hidden_dim must be multiples of 256");
   if (p.NS < 1 || p.NS > kMaxNS) return fail("attention splits out of range");
   if (ncu < 8) return fail("too few compute units");
+  if ((long long)part_weight(ncu) * (p.V > p.hid ? p.V : p.hid) >= (1ll << 32)) return fail("grid x rows exceeds 32 bits");
   if (p.q8 && p.q8 != 64) return fail("int8 group size must be 64");
   if (5 * p.L + 1 >= 4096) return fail("too many layers for the phase tags");
   // every block must own work in every phase: a hand-off buffer may be rewritten as soon as
   // the next phase's outputs are complete, which then implies every block has staged it
-  if (p.dim < ncu || (p.dim + 2 * p.kvd) / 2 < ncu || p.hid < ncu) return fail("model too small for the grid");
+  auto owns = [&](long long n) {  // the partition of geo(): every block's share non-empty
+    for (int b = 0; b < ncu; ++b)
+      if (n * part_weight(b + 1) / part_weight(ncu) == n * part_weight(b) / part_weight(ncu)) return false;
+    return true;
+  };
+  if (!owns(p.dim) || !owns((p.dim + 2 * p.kvd) / 2) || !owns(p.hid)) return fail("model too small for the grid");
   auto nchunks = [&](int K) { return p.q8 ? (K + 4095) / 4096 : (K + PL * 256 - 1) / (PL * 256); };
   auto padf = [&](int K) { return p.q8 ? K : nchunks(K) * PL * 256; };
-  auto nrc = [&](int K, int n_items, int rpi) { return ((n_items + ncu - 1) / ncu) * rpi * nchunks(K); };
+  auto nrc = [&](int K, int n_items, int rpi) {
+    return (int)((long long)n_items * (100 + kXcdSkew) / part_weight(ncu) + 2) * rpi * nchunks(K);
+  };
   p.pad_floats = padf(p.dim) > padf(p.hid) ? padf(p.dim) : padf(p.hid);
   p.q8_pad = p.q8 ? 4096 * (nchunks(p.dim) > nchunks(p.hid) ? nchunks(p.dim) : nchunks(p.hid)) : 0;
   if (nrc(p.dim, (p.dim + 2 * p.kvd) / 2, 2) > kPResFloats || nrc(p.dim, p.hid, 2) > kPResFloats ||
       nrc(p.hid, p.dim, 1) > kPResFloats || nrc(p.dim, p.V, 1) > kPResFloats)
     return fail("too many rows per block");
-  if ((p.dim + ncu - 1) / ncu > kPResidFloats) return fail("residual slice per block too large");
+  if ((long long)p.dim * (100 + kXcdSkew) / part_weight(ncu) + 2 > kPResidFloats)
+    return fail("residual slice per block too large");
   if (lds_bytes(p) > 160 * 1024) return fail("activations do not fit the LDS");
   static bool attr_set = false;
   if (!attr_set) {  // allow more than 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)

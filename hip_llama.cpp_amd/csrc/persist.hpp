@@ -23,7 +23,7 @@ struct PStep {
   unsigned long long* bmax; // [grid] per-block classifier argmax
   int argmax;               // run the argmax + advance tail
   int pad_floats;           // LDS activation strip (floats), >= every phase's padded K
-  unsigned long long* trace; // optional [grid][5L+1][4] timeline (100-MHz clock), or null
+  unsigned long long* trace; // optional [grid][5L+1][kTraceSlots] timeline (100-MHz clock), or null
   // Q8_0 weights (runq.c layout, include/thaQ8.hpp) instead of the fp32 matrices: group size
   // (64; 0 = fp32); per tensor (wq, wk, wv, wo, w1, w2, w3) the layer-0 int8 block and the
   // byte stride between layers, each layer's fp32 scales directly after its int8 block (the
@@ -40,6 +40,7 @@ struct PStep {
 
 constexpr int kPSyncWords = 8 * 32;   // 8 shard counters, one 128-B line each
 constexpr int kPResFloats = 1024;     // per-block row-chunk results (LDS)
+constexpr int kTraceSlots = 12;       // timeline stamps per block and phase (PStep::trace)
 
 // Host: can this step run as one launch on `ncu` co-resident blocks?  Sets pad_floats.
 bool persistent_prepare(PStep& p, int ncu, const char** why);

@@ -171,7 +171,13 @@ __global__ void __launch_bounds__(256) k_q8_quantize(int8_t* q, float* s, const 
     for (int i = 0; i < gs; ++i) wmax = fmaxf(wmax, fabsf(xg[i]));
     const float scale = __fdiv_rn(wmax, 127.0f);
     s[(long long)b * ng + g] = scale;
-    for (int i = 0; i < gs; ++i) q[(long long)b * n + (long long)g * gs + i] = (int8_t)tl::q8_round(__fdiv_rn(xg[i], scale));
+    int8_t* qg = q + (long long)b * n + (long long)g * gs;
+    if (tl::q8_fast_scale(scale)) {  // the hot-path quotient (q8_pack16), exercised by the op tests
+      const float r = __fdiv_rn(1.0f, scale);
+      for (int i = 0; i < gs; ++i) qg[i] = (int8_t)tl::q8_round(tl::q8_div_fast(xg[i], scale, r));
+    } else {
+      for (int i = 0; i < gs; ++i) qg[i] = (int8_t)tl::q8_round(__fdiv_rn(xg[i], scale));
+    }
   }
 }
 

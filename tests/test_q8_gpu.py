@@ -57,6 +57,29 @@ def test_activation_quantisation_bitexact(gpu, handle, oracle, n, gs, B):
         np.testing.assert_array_equal(q[b], qr)
 
 
+@pytest.mark.parametrize("gs", [32, 64])
+def test_activation_quantisation_ties_bitexact(gpu, handle, oracle, gs):
+    """Quotients x / scale at and next to half-integers (the codes where a reciprocal-multiply
+    would round differently): the reciprocal + exact-remainder quotient must equal runq's division."""
+    r = rng(7 * gs)
+    n, B = 64 * gs, 2
+    m = (np.exp(r.uniform(-6, 4, size=(B, n // gs, 1)))).astype(np.float32)
+    j = r.integers(-127, 127, size=(B, n // gs, gs)).astype(np.float32) + 0.5
+    x = (j * (m / np.float32(127.0))).astype(np.float32)
+    nudge = r.integers(-2, 3, size=x.shape)
+    x = np.nextafter(x, np.where(nudge > 0, np.inf, -np.inf).astype(np.float32)).astype(np.float32) * (nudge != 0) + x * (nudge == 0)
+    x[:, :, 0] = m[:, :, 0]  # the group max -> scale = m / 127
+    x = x.reshape(B, n).astype(np.float32)
+    dx, dq, ds = dev(gpu, x), gpu.DevBuf(B * n), gpu.DevBuf(B * (n // gs) * 4)
+    assert gpu.lib().thaBLAS_q8_quantize_batch(C.byref(handle), B, C.cast(C.c_void_p(dq.ptr), C.POINTER(C.c_int8)),
+                                               ds.fptr(), dx.fptr(), n, gs, n) == 0
+    gpu.sync()
+    q = dq.download(np.int8).reshape(B, n)
+    for b in range(B):
+        qr, _ = oracle.q8_quantize(x[b], gs)
+        np.testing.assert_array_equal(q[b], qr)
+
+
 @pytest.mark.parametrize("M,K,gs,B", [(4096, 4096, 64, 1), (4096, 11008, 64, 1), (768, 2048, 64, 4),
                                       (1000, 768, 32, 2), (256, 1024, 128, 8), (64, 96, 32, 1)])
 def test_q8_matmul(gpu, handle, oracle, M, K, gs, B):

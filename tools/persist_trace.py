@@ -46,8 +46,9 @@ def main():
     t = dec.ptrace(False).astype(np.int64)
     L = cfg[2]
     nph = 5 * L + 1
-    G = t.size // (nph * 8)
-    t = t.reshape(G, nph, 8)
+    NSL = 12  # kTraceSlots (persist.hpp)
+    G = t.size // (nph * NSL)
+    t = t.reshape(G, nph, NSL)
     t = (t - t[:, 0, 0].min()) * 0.01  # us
     dim, hid, kvd, V = cfg[0], cfg[1], cfg[0] * cfg[4] // cfg[3], cfg[5]
     esz = 4 if args.dtype == "f32" else 1 + 4 / 64  # int8 + one fp32 scale per 64
@@ -95,6 +96,15 @@ def main():
         i = np.median([t[:, ph, 7] - t[:, ph, 6] for ph in phs])
         print(f"{kind:9s}{f:8.2f}{r:8.2f}{i:8.2f}")
         out[kind + "_stream_wave"] = {"first": float(f), "rest": float(r), "issue": float(i)}
+    # inside the staging (us after the control wave's phase start, medians over blocks and layers):
+    # control wave gathered / normalised / staged; streaming wave 0 gathered / staged
+    print(f"{'kind':9s}{'c.gath':>8s}{'c.norm':>8s}{'c.stgd':>8s}{'s.gath':>8s}{'s.stgd':>8s}   (staging, from phase start)")
+    for kind, k in (("qkv", 0), ("wo", 2), ("ffn_up", 3), ("ffn_down", 4)):
+        phs = list(range(k, nph - 1, 5))
+        med = lambda a, b: float(np.median([t[:, ph, a] - t[:, ph, b] for ph in phs]))
+        row = [med(8, 0), med(9, 0), med(1, 0), med(10, 0), med(4, 0)]
+        print(f"{kind:9s}" + "".join(f"{v:8.2f}" for v in row))
+        out[kind + "_staging"] = row
     if args.json:
         with open(args.json, "w") as f:
             json.dump(out, f, indent=1)
