@@ -38,7 +38,19 @@
 
 namespace tl {
 
-constexpr int PW = 9;        // waves per block: 1 control + 8 streaming
+#ifndef PERSIST_NBUF
+#define PERSIST_NBUF 2
+#endif
+// Register slots in flight per streaming wave.  2: 9 waves (3 on one SIMD, <= 168 VGPRs);
+// 4: 8 waves (2 per SIMD, <= 256 VGPRs), i.e. 28 instead of 16 slots in flight per CU.
+constexpr int NBUF = PERSIST_NBUF;
+// Buffers refilled with the next phase's slots before its staging (the rest right after it).
+// A wave's loads return in order, so its granule sweep waits behind what it prefetched: with
+// int8 weights (short phases, the hand-off dominates) one buffer is best (+2.2% over two),
+// with fp32 both (+1.5% over one); deeper buffering (3-4 per wave, 8 waves) lost 1-8%.
+template <bool Q8>
+constexpr int pfn() { return Q8 ? 1 : NBUF; }
+constexpr int PW = NBUF == 2 ? 9 : 8;  // waves per block: 1 control + PW-1 streaming
 constexpr int PT = PW * 64;  // threads per block
 constexpr int PL = 8;        // wave-loads per slot (8 KiB per wave)
 constexpr int NSW = PW - 1;  // streaming waves per block
@@ -311,9 +323,9 @@ TL_DEVICE void consume_slot_q8(const PGeo& g, int slot, int lane, const f4 (&buf
   }
 }
 
-// Stream this wave's slots (sw, sw + NSW, ...), sw = streaming-wave index; A/B already hold
-// the first two.  Every path loads A and B in the same two places, so the register
-// allocator keeps one pair of register sets for the whole step.
+// Stream this wave's slots (sw, sw + NSW, ...), sw = streaming-wave index; the NBUF buffers
+// already hold the first NBUF.  Every path loads the buffers in the same places, so the
+// register allocator keeps one set of NBUF register buffers for the whole step.
 template <bool Q8>
 TL_DEVICE void load_any(const PDesc& d, const PGeo& g, const PStep& p, int slot, int lane, f4 (&buf)[PL],
                         float (&sc)[PL]) {
@@ -339,29 +351,29 @@ TL_DEVICE void consume_any(const PGeo& g, int slot, int lane, const f4 (&buf)[PL
 TL_DEVICE int take_slot(unsigned* ctr, int lane) {
   unsigned v = 0;
   if (lane == 0) v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  return 2 * NSW + (int)__builtin_amdgcn_readlane(v, 0);
+  return NBUF * NSW + (int)__builtin_amdgcn_readlane(v, 0);
 }
 
 template <bool Q8>
 TL_DEVICE void run_gemv(const PDesc& d, const PGeo& g, const PStep& p, int sw, int lane, const f4* xs,
-                        const signed char* xq, const float* xsc, float* res, f4 (&A)[PL], f4 (&B)[PL],
-                        float (&SA)[PL], float (&SB)[PL], unsigned* ctr, unsigned long long* ts) {
-  int sa = sw, sb = sw + NSW;  // the slots A and B hold (the phase's prefetch)
+                        const signed char* xq, const float* xsc, float* res, f4 (&buf)[NBUF][PL],
+                        float (&sc)[NBUF][PL], unsigned* ctr, unsigned long long* ts) {
+  int sl[NBUF];  // the slots the buffers hold (the phase's prefetch: sw, sw + NSW, ...)
+#pragma unroll
+  for (int i = 0; i < NBUF; ++i) sl[i] = sw + i * NSW;
   bool first = true;
-  // sched_barrier: keep each refill behind the slot's last use (no third register set)
-  while (sa < g.nslot) {
-    consume_any<Q8>(g, sa, lane, A, SA, xs, xq, xsc, res);
-    if (ts && first && lane == 0) *ts = __builtin_amdgcn_s_memrealtime();  // first slot landed
-    first = false;
-    __builtin_amdgcn_sched_barrier(0);
-    sa = take_slot(ctr, lane);
-    if (sa < g.nslot) load_any<Q8>(d, g, p, sa, lane, A, SA);
-    __builtin_amdgcn_sched_barrier(0);
-    if (sb < g.nslot) consume_any<Q8>(g, sb, lane, B, SB, xs, xq, xsc, res);
-    __builtin_amdgcn_sched_barrier(0);
-    sb = take_slot(ctr, lane);
-    if (sb < g.nslot) load_any<Q8>(d, g, p, sb, lane, B, SB);
-    __builtin_amdgcn_sched_barrier(0);
+  // sched_barrier: keep each refill behind the slot's last use (no extra register set)
+  while (sl[0] < g.nslot) {
+#pragma unroll
+    for (int i = 0; i < NBUF; ++i) {
+      if (sl[i] < g.nslot) consume_any<Q8>(g, sl[i], lane, buf[i], sc[i], xs, xq, xsc, res);
+      if (i == 0 && ts && first && lane == 0) *ts = __builtin_amdgcn_s_memrealtime();  // first slot landed
+      first = false;
+      __builtin_amdgcn_sched_barrier(0);
+      sl[i] = take_slot(ctr, lane);
+      if (sl[i] < g.nslot) load_any<Q8>(d, g, p, sl[i], lane, buf[i], sc[i]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
 }
 
@@ -610,14 +622,15 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
     }
   } else {
     const int sw = wave - 1;
-    f4 A[PL], B[PL];
-    float SA[PL], SB[PL];  // Q8 weight scales (unused for fp32)
+    f4 buf[NBUF][PL];
+    float sc[NBUF][PL];  // Q8 weight scales (unused for fp32)
     __syncthreads();  // first norm weights preloaded
     {
       const PDesc d0 = make_desc<Q8>(p, p.L > 0 ? PK_QKV : PK_CLS, p.L > 0 ? 0 : p.L, tb);
       const PGeo g0 = geo<Q8>(d0);
-      load_any<Q8>(d0, g0, p, sw, lane, A, SA);
-      load_any<Q8>(d0, g0, p, sw + NSW, lane, B, SB);
+#pragma unroll
+      for (int i = 0; i < NBUF; ++i)
+        if (sw + i * NSW < g0.nslot) load_any<Q8>(d0, g0, p, sw + i * NSW, lane, buf[i], sc[i]);
     }
     for (int ph = 0; ph < nph; ++ph) {
       const int l = ph / 5;
@@ -629,7 +642,12 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
       stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, wave, lane,
                 tr ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots : nullptr);
       if (tr) TRACE(4);
-      run_gemv<Q8>(d, g, p, sw, lane, xs, xq, xsc, res, A, B, SA, SB, ctr,
+      if (ph > 0) {  // the buffers not prefetched across the phase boundary
+#pragma unroll
+        for (int i = pfn<Q8>(); i < NBUF; ++i)
+          if (sw + i * NSW < g.nslot) load_any<Q8>(d, g, p, sw + i * NSW, lane, buf[i], sc[i]);
+      }
+      run_gemv<Q8>(d, g, p, sw, lane, xs, xq, xsc, res, buf, sc, ctr,
                    tr ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots + 5 : nullptr);
       if (tr) TRACE(6);
       // every slot reduced into res: the control wave's epilogue (the hand-off every other
@@ -638,8 +656,9 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
       if (kind != PK_CLS) {
         const PDesc nd = next_desc<Q8>(p, kind, l, tb);
         const PGeo ng = geo<Q8>(nd);
-        if (sw < ng.nslot) load_any<Q8>(nd, ng, p, sw, lane, A, SA);
-        if (sw + NSW < ng.nslot) load_any<Q8>(nd, ng, p, sw + NSW, lane, B, SB);
+#pragma unroll
+        for (int i = 0; i < pfn<Q8>(); ++i)
+          if (sw + i * NSW < ng.nslot) load_any<Q8>(nd, ng, p, sw + i * NSW, lane, buf[i], sc[i]);
       }
       if (tr) TRACE(7);
     }
