@@ -479,11 +479,19 @@ TL_DEVICE void preload_rms(const float* w, int dim, float* rmsw, int lane) {
   for (int j = lane; j < (dim >> 2); j += 64) d4[j] = s4[j];
 }
 
+// (cos, sin) of the RoPE pair at QKV row `row` (< dim + kv_dim) for this step's position.
+TL_DEVICE float2 rope_cs(const PStep& p, int row) {
+  const int i = row < p.dim ? row : row - p.dim;
+  return p.rope[(long long)p.pos[0] * (p.hs >> 1) + ((i % p.hs) >> 1)];
+}
+
 // Control wave: row values from the LDS row-chunk sums, fused epilogue, granule stores.
+// cs0: the RoPE (cos, sin) of this lane's first QKV item, loaded while the slots streamed
+// (a table read at the epilogue put one L2 round trip on every layer's critical path).
 // xres: this block's slice of the residual stream x (rows i0.. of the dim-row phases, the
 // same slice for Wo and W2), kept in LDS so the residual add never re-reads x.
 TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const float* res, float* xres, int lane,
-                        int l) {
+                        int l, float2 cs0) {
   unsigned long long best = 0;
   for (int it = lane; it < g.ni; it += 64) {
     float v[2] = {0.f, 0.f};
@@ -509,8 +517,7 @@ TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const flo
       const int pb = p.pos[0];
       float a0 = v[0], a1 = v[1];
       if (row < p.dim + p.kvd) {
-        const int i = row < p.dim ? row : row - p.dim;
-        const float2 cs = p.rope[(long long)pb * (p.hs >> 1) + ((i % p.hs) >> 1)];
+        const float2 cs = it == lane ? cs0 : rope_cs(p, row);
         const float r0 = __fsub_rn(__fmul_rn(a0, cs.x), __fmul_rn(a1, cs.y));
         const float r1 = __fadd_rn(__fmul_rn(a0, cs.y), __fmul_rn(a1, cs.x));
         a0 = r0; a1 = r1;
@@ -612,12 +619,16 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
       stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, wave, lane,
                 p.trace ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots : nullptr);
       TRACE(1);
-      if (kind == PK_QKV) preload_rms(p.rms_ffn + (long long)l * p.dim, p.dim, rmsw, lane);
+      float2 cs0 = make_float2(1.f, 0.f);
+      if (kind == PK_QKV) {
+        preload_rms(p.rms_ffn + (long long)l * p.dim, p.dim, rmsw, lane);
+        if (lane < g.ni && 2 * (g.i0 + lane) < p.dim + p.kvd) cs0 = rope_cs(p, 2 * (g.i0 + lane));
+      }
       if (kind == PK_UP) preload_rms(l + 1 < p.L ? p.rms_att + (long long)(l + 1) * p.dim : p.rms_final, p.dim, rmsw, lane);
       __syncthreads();  // every slot reduced into res
       if (lane == 0) *ctr = 0u;  // next GEMV phase's slot counter (used after its staging barrier)
       TRACE(2);
-      epilogue(d, g, p, res, xres, lane, l);
+      epilogue(d, g, p, res, xres, lane, l, cs0);
       TRACE(3);
     }
   } else {
@@ -642,7 +653,8 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
       stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, wave, lane,
                 tr ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots : nullptr);
       if (tr) TRACE(4);
-      if (ph > 0) {  // the buffers not prefetched across the phase boundary
+      if (ph > 0) {  // the buffers not prefetched across the phase boundary (issuing them after
+                     // the first slot's consume instead lost 2.5% int8)
 #pragma unroll
         for (int i = pfn<Q8>(); i < NBUF; ++i)
           if (sw + i * NSW < g.nslot) load_any<Q8>(d, g, p, sw + i * NSW, lane, buf[i], sc[i]);
