@@ -117,9 +117,11 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p) {
 // Wave-level decode attention: one 64-lane wave (= one 64-thread block) per
 // (sequence b, head h, unit s), NS units per (b, h).  Unit s walks key chunks
 // c = s, s+NS, s+2NS, ... of CH keys; for every chunk the K rows AND the V rows
-// are requested together (one memory latency per chunk, not three), the
-// scores go through a 32-float LDS strip, and chunks are merged with an online
-// softmax.  No block barriers: max/sum are wave reductions.
+// are requested together (one memory latency per chunk, not three), key t's
+// score lands in lane t (DPP row sums + readlane + lane select, no LDS strip), and
+// chunks are merged with an online softmax.  No block barriers: max/sum are
+// DPP wave reductions (the ds_bpermute forms put an LDS round trip per step on
+// the decode critical path).
 //  * if the context fits one chunk (T <= CH) unit 0 alone computes the reference
 //    order exactly (normalise the probabilities, then sum) and writes the output;
 //  * otherwise each live unit publishes (o, m, l) with write-through (sc1)
@@ -142,6 +144,7 @@ struct AttnWaveParams {
   unsigned long long* gout;        // [dim]
   unsigned tag_in, tag_out;
   unsigned* err;
+  unsigned long long* ts;          // optional timeline (persistent step trace): q ready, k/v ready, done
 };
 
 TL_DEVICE void st_sc1(float* p, float v) { st1_sc1(p, v); }
@@ -151,8 +154,8 @@ TL_DEVICE float ld_sc1(const float* p) { return ld1_sc1(p); }
 // wave retire in order, this only stops the compiler from moving them.
 TL_DEVICE void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// The body of one attention unit, run by one full wave.  `sc` is this wave's private
-// 64-float LDS strip; `unit` must be wave-uniform.  Also used inside the persistent step
+// The body of one attention unit, run by one full wave.  `sc` (a 64-float LDS strip) is no
+// longer used; `unit` must be wave-uniform.  Also used inside the persistent step
 // kernel (persist.hip) with GR = true: q and the K/V rows at position pos come from the
 // granules the QKV phase of the same launch published (rows < pos were written by earlier
 // launches and are read from the cache), and the output is published as granules.
@@ -215,6 +218,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane)
       if (!qready) {
         qv = gran_wait4(rg, (unsigned)(h * HS + (lane % LPK) * 4) * 8u, w.tag_in, w.err);
         qready = true;
+        if (w.ts && lane == 0) w.ts[0] = __builtin_amdgcn_s_memrealtime();
       }
       if (t1 == T) {  // this chunk holds the new row
         const unsigned kofs = (unsigned)(p.dim + kvh * HS), vofs = (unsigned)(p.dim + p.kv_dim + kvh * HS);
@@ -222,6 +226,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane)
         float vn[VPL];
 #pragma unroll
         for (int c = 0; c < VPL; ++c) vn[c] = gran_wait(w.gqkv + vofs + lane * VPL + c, w.tag_in, w.err);
+        if (w.ts && lane == 0) w.ts[1] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
         for (int i = 0; i < NI; ++i)
           if (min(t0 + i * KPI + lane / LPK, t1 - 1) == T - 1) kv[i] = kn;
@@ -245,28 +250,34 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane)
         for (int c = 0; c < VPL; ++c) vv[u][c] = vr[c];
       }
     }
-    // scores (reference src/seq.cpp:107-117)
+    // scores (reference src/seq.cpp:107-117): row sums by DPP, a key's rows added through
+    // SGPRs, key t's score written into lane t (no LDS strip, no ds_bpermute round trips)
+    constexpr int R = LPK / 16;  // 16-lane rows per key row
+    float raw = 0.f;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const float d = group_sum<LPK>(dot4(qv, kv[i], 0.f));
-      const int t = i * KPI + lane / LPK;
-      if ((lane % LPK) == 0 && t < n) sc[t] = __fdiv_rn(d, rs);
+      const float d = row16_sum(dot4(qv, kv[i], 0.f));
+#pragma unroll
+      for (int j = 0; j < KPI; ++j) {
+        float sj = lane_f(d, 16 * j * R);
+#pragma unroll
+        for (int r = 1; r < R; ++r) sj += lane_f(d, 16 * (j * R + r));
+        raw = lane == i * KPI + j ? sj : raw;
+      }
     }
-    wave_lds_fence();  // score strip written
-    const float my = lane < n ? sc[lane] : -3.402823466e+38f;
-    wave_lds_fence();  // the strip is rewritten by the next chunk
-    const float mc = wave_max(my);
+    const float my = lane < n ? __fdiv_rn(raw, rs) : -3.402823466e+38f;
+    const float mc = wave_max_u(my);
     float pr;
     if (whole) {
       // reference softmax (src/seq.cpp:18-36): exp, sum, divide, then the weighted sum
       const float e = lane < n ? expf(__fsub_rn(my, mc)) : 0.f;
-      pr = __fdiv_rn(e, wave_sum(e));
+      pr = __fdiv_rn(e, wave_sum_u(e));
       m = mc;
     } else {
       const float mn = fmaxf(m, mc);
       const float e = lane < n ? expf(__fsub_rn(my, mn)) : 0.f;
       const float scale = expf(__fsub_rn(m, mn));  // rescale what earlier chunks summed
-      l = fmaf(l, scale, wave_sum(e));
+      l = fmaf(l, scale, wave_sum_u(e));
 #pragma unroll
       for (int c = 0; c < VPL; ++c) o[c] *= scale;
       m = mn;
@@ -274,7 +285,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane)
     }
 #pragma unroll
     for (int u = 0; u < CH; ++u) {
-      const float a = __shfl(pr, u, 64);
+      const float a = lane_f(pr, u);
 #pragma unroll
       for (int c = 0; c < VPL; ++c) o[c] = fmaf(a, vv[u][c], o[c]);
     }
@@ -283,6 +294,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane)
   float* out = p.out + (long long)b * p.dim + h * HS + lane * VPL;
   if (whole) {
     if constexpr (GR) {
+      if (w.ts && lane == 0) w.ts[2] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
       for (int c = 0; c < VPL; ++c) st8_sc1(w.gout + h * HS + lane * VPL + c, gran(w.tag_out, o[c]));
     } else {
@@ -302,7 +314,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   unsigned ticket = 0;
   if (lane == 0) ticket = __hip_atomic_fetch_add(w.cnt + bh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  ticket = __shfl(ticket, 0, 64);
+  ticket = (unsigned)__builtin_amdgcn_readfirstlane((int)ticket);
   if (ticket != (unsigned)(nact - 1)) return;
   // last unit: combine every partial (sc1 loads only).  Lane k reads unit k's (m, l);
   // every lane then reads its columns of all kMaxNS records at once (records past nact
@@ -319,15 +331,15 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane)
 #pragma unroll
     for (int c = 0; c < VPL; ++c) ov[k][c] = ld_sc1(recs + kk * (HS + 4) + lane * VPL + c);
   }
-  const float M = wave_max(lane < nact ? mk : -3.402823466e+38f);
+  const float M = wave_max_u(lane < nact ? mk : -3.402823466e+38f);
   const float sk = lane < nact ? expf(__fsub_rn(mk, M)) : 0.f;
-  const float L = wave_sum(lk * sk);
+  const float L = wave_sum_u(lk * sk);
   float acc[VPL];
 #pragma unroll
   for (int c = 0; c < VPL; ++c) acc[c] = 0.f;
 #pragma unroll
   for (int k = 0; k < kMaxNS; ++k) {
-    const float a = __shfl(sk, k, 64);
+    const float a = lane_f(sk, k);
 #pragma unroll
     for (int c = 0; c < VPL; ++c) acc[c] = fmaf(ov[k][c], a, acc[c]);
   }

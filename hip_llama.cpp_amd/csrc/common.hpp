@@ -27,6 +27,36 @@ TL_DEVICE float wave_max(float v) {
   return v;
 }
 
+// DPP lane moves (VALU, no LDS round trip; GFX9 encodings): quad_perm [1,0,3,2] = 0xB1,
+// quad_perm [2,3,0,1] = 0x4E, row_half_mirror = 0x141, row_mirror = 0x140.  The __shfl_xor
+// forms above lower to ds_bpermute (an LDS round trip per step); these are for latency-bound
+// reductions on the decode critical path.  All 64 lanes must be active.
+template <int CTRL>
+TL_DEVICE float dpp_f(float v) { return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false)); }
+TL_DEVICE float lane_f(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+// Sum over each 16-lane row; every lane of the row holds it.
+TL_DEVICE float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  return v + dpp_f<0x140>(v);
+}
+TL_DEVICE float row16_max(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  return fmaxf(v, dpp_f<0x140>(v));
+}
+// Wave-uniform sum / max: row reductions by DPP, the four rows combined through SGPRs.
+TL_DEVICE float wave_sum_u(float v) {
+  v = row16_sum(v);
+  return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
+}
+TL_DEVICE float wave_max_u(float v) {
+  v = row16_max(v);
+  return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
+}
+
 // Sum over the first `width` lanes groups (width power of two <= 64): lanes
 // [g*width, (g+1)*width) end up holding their group's total.
 template <int WIDTH>

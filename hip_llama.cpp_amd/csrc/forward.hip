@@ -436,7 +436,7 @@ static int enqueue_step(thallama_decoder* d) {
       int ev = prof_begin(d);
       if (d->hs == 64 || d->hs == 128 || d->hs == 256) {
         // wave-level units, in-kernel combine (attention.hpp: attn_wave_kernel)
-        tl::AttnWaveParams wp;
+        tl::AttnWaveParams wp = {};
         wp.a = a;
         wp.cnt = d->cnt_d;
         wp.B = d->B;

@@ -226,7 +226,7 @@ TL_DEVICE void consume_slot(const PGeo& g, int slot, int lane, const f4 (&buf)[P
     for (int u = q * 4; u < q * 4 + 4; ++u) a = dot4(buf[u], xc[u * 64], a);
     __builtin_amdgcn_sched_barrier(0);
   }
-  a = wave_sum(a);
+  a = wave_sum_u(a);
   if (lane == 0) res[slot] = a;
 }
 
@@ -317,7 +317,7 @@ TL_DEVICE void consume_slot_q8(const PGeo& g, int slot, int lane, const f4 (&buf
     gs += __builtin_amdgcn_mov_dpp(b1 ? s0 : s1, 0x4E, 0xF, 0xF, false);       // quad_perm [2,3,0,1]
     const int grp = c * 64 + (lane & 3) * 16 + (lane >> 2);
     a = __fmul_rn(__fmul_rn((float)gs, sc[h]), xsc[grp]);  // runq.c:334
-    a = wave_sum(a);
+    a = wave_sum_u(a);
     if (lane == 0 && Q < g.nres) res[Q] = a;
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -432,7 +432,7 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, sign
   if (d.rms) {
     // reference rmsnorm (src/seq.cpp:3-16): ss = 1/sqrtf(sum/size + 1e-5f); the block sum
     // is taken in a fixed order (waves 0..PW-1), so every block gets the same ss
-    sq = wave_sum(sq);
+    sq = wave_sum_u(sq);
     if (lane == 0) red[wave] = sq;
     __syncthreads();
     float t = red[0];
@@ -599,7 +599,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
       TRACE(0);
       if (kind == PK_ATTN) {
         // one wave per (head, key-split) unit: unit u on block u % G
-        AttnWaveParams aw;
+        AttnWaveParams aw = {};
         aw.a.q = p.xb; aw.a.kc = p.kc; aw.a.vc = p.vc;  // (q comes from the granules)
         aw.a.kv_b_stride = (long long)p.L * p.S * p.kvd;
         aw.a.kv_l_off = (long long)l * p.S * p.kvd;
@@ -609,6 +609,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
         aw.cnt = p.tickets + (long long)l * p.H; aw.B = 1; aw.NS = p.NS;
         aw.gqkv = p.gqkv; aw.gout = p.gxb;
         aw.tag_in = tb + 5u * l + 1; aw.tag_out = tb + 5u * l + 2; aw.err = p.err;
+        aw.ts = p.trace ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots + 8 : nullptr;
         const int units = p.H * p.NS;
         for (int u = blockIdx.x; u < units; u += G) attn_unit<HS, 16, true>(aw, u, strips, lane);
         TRACE(3);

@@ -105,6 +105,15 @@ def main():
         row = [med(8, 0), med(9, 0), med(1, 0), med(10, 0), med(4, 0)]
         print(f"{kind:9s}" + "".join(f"{v:8.2f}" for v in row))
         out[kind + "_staging"] = row
+    # attention phase on the blocks that run a unit (single-chunk contexts): q granule ready,
+    # k/v granules ready, output computed, unit done (us after the phase start)
+    att = [ph for ph in range(1, nph - 1, 5)]
+    a = np.stack([t[:, ph, :] for ph in att])  # [layers][G][slots]
+    live = a[:, :, 10] > a[:, :, 0]
+    if live.any():
+        rel = lambda k: float(np.median((a[:, :, k] - a[:, :, 0])[live]))
+        print(f"attention units ({int(live.sum() / len(att))} per layer): q {rel(8):.2f}  kv {rel(9):.2f}  "
+              f"computed {rel(10):.2f}  done {rel(3):.2f} us after phase start")
     if args.json:
         with open(args.json, "w") as f:
             json.dump(out, f, indent=1)
