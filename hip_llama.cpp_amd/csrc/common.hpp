@@ -57,6 +57,18 @@ TL_DEVICE float wave_max_u(float v) {
   return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
 }
 
+// Exact int32 sum over aligned groups of N = 2, 4 or 8 lanes (every lane of a group gets
+// it): quad DPP steps, then row_half_mirror (after the quad steps the two quads of a half-row
+// each hold their sum, so the mirror pairs them).
+template <int N>
+TL_DEVICE int lane_group_sum_i(int v) {
+  static_assert(N == 2 || N == 4 || N == 8, "group of 2, 4 or 8 lanes");
+  v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
+  if constexpr (N >= 4) v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);
+  if constexpr (N >= 8) v += __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false);
+  return v;
+}
+
 // Sum over the first `width` lanes groups (width power of two <= 64): lanes
 // [g*width, (g+1)*width) end up holding their group's total.
 template <int WIDTH>

@@ -346,7 +346,7 @@ __global__ void __launch_bounds__(WAVES * 64) gemv_kernel(GemvParams p, int kc_m
 #pragma unroll
     for (int r = 0; r < 2; ++r)
 #pragma unroll
-      for (int b = 0; b < NB; ++b) v[r][b] = r < RPI ? wave_sum(acc[i][r < RPI ? r : 0][b]) : 0.f;
+      for (int b = 0; b < NB; ++b) v[r][b] = r < RPI ? wave_sum_u(acc[i][r < RPI ? r : 0][b]) : 0.f;
     epilogue<MODE, NB>(p, item, v, lane);
   }
 }
@@ -368,7 +368,7 @@ __global__ void __launch_bounds__(256) gemv_generic_kernel(GemvParams p) {
   if (p.rms_w) {
     float t = 0.f;
     for (int k = lane; k < p.K; k += 64) t = fmaf(xin[k], xin[k], t);
-    t = wave_sum(t);
+    t = wave_sum_u(t);
     s = __fdiv_rn(1.0f, sqrtf(__fadd_rn(__fdiv_rn(t, (float)p.K), 1e-5f)));
   }
   if (p.tok && item == 0 && (threadIdx.x >> 6) == 0)
@@ -382,7 +382,7 @@ __global__ void __launch_bounds__(256) gemv_generic_kernel(GemvParams p) {
       if (p.rms_w) xv = __fmul_rn(p.rms_w[k], __fmul_rn(s, xv));
       a = fmaf(w[k], xv, a);
     }
-    v[r][0] = wave_sum(a);
+    v[r][0] = wave_sum_u(a);
   }
   // reuse the NB=1 epilogue for sequence b by shifting the per-b pointers
   GemvParams q = p;

@@ -202,8 +202,7 @@ TL_DEVICE void q8_dot(q8i4 wv, float wsc, const int8_t* xq, const float* xsc, in
     d = __builtin_amdgcn_sdot4(wv.y, xv.y, d, false);
     d = __builtin_amdgcn_sdot4(wv.z, xv.z, d, false);
     d = __builtin_amdgcn_sdot4(wv.w, xv.w, d, false);
-#pragma unroll
-    for (int o = LPG / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+    d = lane_group_sum_i<LPG>(d);
     // runq.c:334: val += ((float)ival) * w.s * x.s, once per group (its first lane)
     if ((lane % LPG) == 0) acc[b] += __fmul_rn(__fmul_rn((float)d, wsc), xsc[b * ng + gidx]);
   }
@@ -295,7 +294,7 @@ __global__ void __launch_bounds__(WAVES * 64) gemv_q8_kernel(GemvParams p, int k
 #pragma unroll
     for (int r = 0; r < 2; ++r)
 #pragma unroll
-      for (int b = 0; b < NB; ++b) v[r][b] = r < RPI ? wave_sum(acc[i * RPI + (r < RPI ? r : 0)][b]) : 0.f;
+      for (int b = 0; b < NB; ++b) v[r][b] = r < RPI ? wave_sum_u(acc[i * RPI + (r < RPI ? r : 0)][b]) : 0.f;
     epilogue<MODE, NB>(p, item, v, lane);
   }
 }
