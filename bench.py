@@ -224,23 +224,24 @@ def main():
         stp, ffn = prof.get("step"), prof.get("ffn_up")
         # HBM traffic of the same kernel from the committed rocprofv3 PMC passes (FETCH_SIZE and
         # WRITE_SIZE in separate runs, gfx950 FETCH_SIZE x2 correction): profiles/r01_pmc_traffic.json
+        pmc_file = "r01_pmc_traffic_int8.json" if q8 else "r01_pmc_traffic.json"
         pmc = {}
         try:
-            with open(os.path.join(REPO, "profiles", "r01_pmc_traffic.json")) as f:
+            with open(os.path.join(REPO, "profiles", pmc_file)) as f:
                 pmc = json.load(f)["kernels"]
         except (OSError, ValueError, KeyError):
             pmc = {}
 
         def traffic_of(prefix):
-            if mname != "llama2-7B" or q8 or B != 1:
-                return None  # the committed PMC pass was taken on the 7B fp32 batch-1 workload
+            if mname != "llama2-7B" or B != 1:
+                return None  # the committed PMC passes were taken on the 7B batch-1 workloads
             hits = [v["traffic_bytes"] for k, v in pmc.items() if k.startswith(prefix)]
             return round(hits[0]) if hits else None
         if stp:
             roof = {"bound": "hbm", "achieved": round(stp["GBps"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(stp["GBps"] / HBM_PEAK_GBS, 4),
                     "traffic": traffic_of("void tl::persistent_step_kernel<"),
-                    "traffic_source": "profiles/r01_pmc_traffic.json (rocprofv3 --pmc, positions 0..1)",
+                    "traffic_source": f"profiles/{pmc_file} (rocprofv3 --pmc, positions 0..1)",
                     "kernel": "persistent_step_kernel (the whole decode step, one launch)",
                     "bytes_per_launch": step_bytes_p, "avg_us": round(stp["avg_us"], 2),
                     "positions": f"0..{P - 1}"}
@@ -248,7 +249,7 @@ def main():
             roof = {"bound": "hbm", "achieved": round(ffn["GBps"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ffn["GBps"] / HBM_PEAK_GBS, 4),
                     "traffic": None if q8 else traffic_of("void tl::gemv_kernel<2, 1, 1, true, 4, false>"),
-                    "traffic_source": "profiles/r01_pmc_traffic.json (rocprofv3 --pmc)",
+                    "traffic_source": f"profiles/{pmc_file} (rocprofv3 --pmc)",
                     "kernel": ("gemv_q8_kernel" if q8 else "gemv_kernel") + "<GM_SWIGLU> (RMSNorm + W1/W3 + SwiGLU)",
                     "bytes_per_launch": launch_bytes(tl.K_FFN_UP, [0] * B), "avg_us": round(ffn["avg_us"], 2)}
         out = {
