@@ -44,24 +44,40 @@ TL_DEVICE float q8_div_fast(float x, float scale, float r) {
   const float y = __fmul_rn(x, r);
   return __builtin_fmaf(__builtin_fmaf(-y, scale, x), r, y);
 }
-TL_DEVICE q8i4 q8_pack16(const f4 (&v)[4], float scale) {
-  float q[16];
+template <int NF4>  // NF4 float4s -> NF4 dwords of int8 codes
+TL_DEVICE void q8_pack(const f4 (&v)[NF4], float scale, int (&packed)[NF4]) {
+  float q[4 * NF4];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) { q[4 * u] = v[u].x; q[4 * u + 1] = v[u].y; q[4 * u + 2] = v[u].z; q[4 * u + 3] = v[u].w; }
+  for (int u = 0; u < NF4; ++u) { q[4 * u] = v[u].x; q[4 * u + 1] = v[u].y; q[4 * u + 2] = v[u].z; q[4 * u + 3] = v[u].w; }
+  int qi[4 * NF4];
   if (q8_fast_scale(scale)) {
+    // |x / scale| <= 127 (1 + 2^-23) here, and for |y| <= 200 round-half-away-from-zero is
+    // the truncation of y + copysign(pred(0.5), y) (all 2.26e9 such floats: tools/probes/q8round.c)
     const float r = __fdiv_rn(1.0f, scale);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) q[i] = q8_div_fast(q[i], scale, r);
+    for (int i = 0; i < 4 * NF4; ++i) {
+      const float y = q8_div_fast(q[i], scale, r);
+      qi[i] = (int)__fadd_rn(y, __builtin_copysignf(0.49999997f, y));
+    }
   } else {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) q[i] = __fdiv_rn(q[i], scale);
+    for (int i = 0; i < 4 * NF4; ++i) qi[i] = q8_round(__fdiv_rn(q[i], scale));
   }
-  q8i4 packed;
 #pragma unroll
-  for (int u = 0; u < 4; ++u)
-    packed[u] = (q8_round(q[4 * u]) & 0xFF) | ((q8_round(q[4 * u + 1]) & 0xFF) << 8) |
-                ((q8_round(q[4 * u + 2]) & 0xFF) << 16) | ((q8_round(q[4 * u + 3]) & 0xFF) << 24);
-  return packed;
+  for (int u = 0; u < NF4; ++u)
+    packed[u] = (qi[4 * u] & 0xFF) | ((qi[4 * u + 1] & 0xFF) << 8) | ((qi[4 * u + 2] & 0xFF) << 16) |
+                ((qi[4 * u + 3] & 0xFF) << 24);
+}
+typedef int q8i2 __attribute__((ext_vector_type(2)));
+TL_DEVICE q8i4 q8_pack16(const f4 (&v)[4], float scale) {
+  int p[4];
+  q8_pack<4>(v, scale, p);
+  return q8i4{p[0], p[1], p[2], p[3]};
+}
+TL_DEVICE q8i2 q8_pack8(const f4 (&v)[2], float scale) {
+  int p[2];
+  q8_pack<2>(v, scale, p);
+  return q8i2{p[0], p[1]};
 }
 
 TL_DEVICE f4 rms_apply(f4 v, f4 w, float s) {

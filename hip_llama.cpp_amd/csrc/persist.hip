@@ -429,6 +429,7 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, sign
     gather<SB>(rsrc_of(d.gin), d.tag_in, n4, pad4, threadIdx.x, PT, xs, sq, p.err);
   }
   if (ts && lane == 0) ts[wave == 0 ? 8 : 10] = __builtin_amdgcn_s_memrealtime();  // input gathered
+  float ss = 1.f;
   if (d.rms) {
     // reference rmsnorm (src/seq.cpp:3-16): ss = 1/sqrtf(sum/size + 1e-5f); the block sum
     // is taken in a fixed order (waves 0..PW-1), so every block gets the same ss
@@ -438,34 +439,35 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, sign
     float t = red[0];
 #pragma unroll
     for (int w = 1; w < PW; ++w) t += red[w];
-    const float s = __fdiv_rn(1.0f, sqrtf(__fadd_rn(__fdiv_rn(t, (float)d.K), 1e-5f)));
-    const f4* w4 = reinterpret_cast<const f4*>(rmsw);
-    for (int j = threadIdx.x; j < n4; j += PT) {
-      const f4 w = w4[j];
-      const f4 v = xs[j];
-      xs[j] = f4{__fmul_rn(w.x, __fmul_rn(s, v.x)), __fmul_rn(w.y, __fmul_rn(s, v.y)),
-                 __fmul_rn(w.z, __fmul_rn(s, v.z)), __fmul_rn(w.w, __fmul_rn(s, v.w))};
+    ss = __fdiv_rn(1.0f, sqrtf(__fadd_rn(__fdiv_rn(t, (float)d.K), 1e-5f)));
+    if constexpr (!Q8) {
+      const f4* w4 = reinterpret_cast<const f4*>(rmsw);
+      for (int j = threadIdx.x; j < n4; j += PT) xs[j] = rms_apply(xs[j], w4[j], ss);
     }
   }
   if (ts && lane == 0 && wave == 0) ts[9] = __builtin_amdgcn_s_memrealtime();  // normalised
   if constexpr (Q8) {
-    // runq.c:145-171 quantize over the padded strip: 4 consecutive threads (one quad) per
-    // group of 64, 16 values each; scale = max|x| / 127, q = round(x / scale)
-    __syncthreads();
-    const int nsl = g.nch * 256;
+    // runq.c:145-171 quantize over the padded strip (the RMSNorm applied on the fly, same
+    // arithmetic as the fp32 strip): 8 consecutive threads per group of 64, 8 values each;
+    // scale = max|x| / 127, q = round(x / scale)
+    if (!d.rms) __syncthreads();  // (with a norm, the sum's barrier already ordered the sweep)
+    const f4* w4 = reinterpret_cast<const f4*>(rmsw);
+    const int nsl = g.nch * 512;
     for (int sl = threadIdx.x; sl < nsl; sl += PT) {
-      f4 v[4];
+      f4 v[2];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = sl * 4 + u < n4 ? xs[sl * 4 + u] : f4{0.f, 0.f, 0.f, 0.f};
-      float m = 0.f;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
-      m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0xB1, 0xF, 0xF, false)));
-      m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0x4E, 0xF, 0xF, false)));
+      for (int u = 0; u < 2; ++u) {
+        const int j = sl * 2 + u;
+        v[u] = j < n4 ? (d.rms ? rms_apply(xs[j], w4[j], ss) : xs[j]) : f4{0.f, 0.f, 0.f, 0.f};
+      }
+      float m = fmaxf(fmaxf(fmaxf(fabsf(v[0].x), fabsf(v[0].y)), fmaxf(fabsf(v[0].z), fabsf(v[0].w))),
+                      fmaxf(fmaxf(fabsf(v[1].x), fabsf(v[1].y)), fmaxf(fabsf(v[1].z), fabsf(v[1].w))));
+      m = fmaxf(m, dpp_f<0xB1>(m));
+      m = fmaxf(m, dpp_f<0x4E>(m));
+      m = fmaxf(m, dpp_f<0x141>(m));  // row_half_mirror: the two quads of the group
       const float scale = __fdiv_rn(m, 127.0f);
-      *reinterpret_cast<q8i4*>(xq + sl * 16) = q8_pack16(v, scale);
-      if ((sl & 3) == 0) xsc[sl >> 2] = scale;
+      *reinterpret_cast<q8i2*>(xq + sl * 8) = q8_pack8(v, scale);
+      if ((sl & 7) == 0) xsc[sl >> 3] = scale;
     }
   }
   __syncthreads();
