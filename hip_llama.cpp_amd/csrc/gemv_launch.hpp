@@ -113,8 +113,15 @@ inline hipError_t launch_mode(const GemvParams& p0, hipStream_t s, const GemvCfg
       const int tiles = (rows + 15) / 16;
       mfma_splits(p, tiles);
       const dim3 grid(tiles * p.msplit);
-      if (c.nt) hipLaunchKernelGGL((gemv_mfma_kernel<MODE, true>), grid, dim3(kMfmaWaves * 64), 0, s, p);
-      else hipLaunchKernelGGL((gemv_mfma_kernel<MODE, false>), grid, dim3(kMfmaWaves * 64), 0, s, p);
+      // activation load instructions per 16-row group (4 rows each): only those with live rows
+      const dim3 blk(kMfmaWaves * 64);
+      if (p.nb <= 8) {
+        if (c.nt) hipLaunchKernelGGL((gemv_mfma_kernel<MODE, true, 2>), grid, blk, 0, s, p);
+        else hipLaunchKernelGGL((gemv_mfma_kernel<MODE, false, 2>), grid, blk, 0, s, p);
+      } else {
+        if (c.nt) hipLaunchKernelGGL((gemv_mfma_kernel<MODE, true, 4>), grid, blk, 0, s, p);
+        else hipLaunchKernelGGL((gemv_mfma_kernel<MODE, false, 4>), grid, blk, 0, s, p);
+      }
       e = hipGetLastError();
     } else if (p.nb == 1) e = launch_nb<MODE, 1>(p, s, c);
     else if (p.nb == 2) e = launch_nb<MODE, 2>(p, s, c);

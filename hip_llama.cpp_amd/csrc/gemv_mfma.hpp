@@ -101,7 +101,7 @@ static __global__ void __launch_bounds__(256) gemv_prenorm_kernel(GemvParams p) 
 // r01_mfma_sweep.jsonl); LDS traffic is ~1 B per weight byte.  The weights of group g + 1
 // are in flight while group g multiplies; steps past the run load a clamped (valid)
 // address and multiply zero activations, so no load is predicated.
-template <int MODE, bool NT>
+template <int MODE, bool NT, int XI>
 __global__ void __launch_bounds__(kMfmaWaves * 64) gemv_mfma_kernel(GemvParams p) {
   constexpr int W = kMfmaWaves;
   constexpr bool TWO = MODE == GM_SWIGLU;
@@ -110,6 +110,7 @@ __global__ void __launch_bounds__(kMfmaWaves * 64) gemv_mfma_kernel(GemvParams p
   constexpr int LPR = U * 4;           // lanes per row in a load (16 B each): 256-B runs
   constexpr int RPI = 64 / LPR;        // rows per load instruction
   constexpr int NI = 16 / RPI;         // load instructions per 16-row tile
+  static_assert(XI >= 1 && XI <= NI, "live activation load instructions");
   constexpr int STR = U * 16 + 4;      // LDS row stride in floats (padded)
   constexpr int TILE = 16 * STR;       // floats per tile
   __shared__ __attribute__((aligned(16))) float lds[W * (NR + 1) * TILE];
@@ -161,6 +162,10 @@ __global__ void __launch_bounds__(kMfmaWaves * 64) gemv_mfma_kernel(GemvParams p
     if constexpr (NT) return __builtin_nontemporal_load(a);
     else return *a;
   };
+  // activation rows >= nb are zero: only the first XI of the NI activation load instructions
+  // are issued (XI * RPI >= nb, a compile-time count: a run-time skip made the compiler's
+  // vmcnt waits conservative), the other tile rows stay zero from the start
+  auto xlive = [&](int v) { return v < XI; };
   auto load = [&](f4 (&t)[NR + 1][NI], int g) {
     bool ok;
     const int k = kof(g, ok);
@@ -168,11 +173,16 @@ __global__ void __launch_bounds__(kMfmaWaves * 64) gemv_mfma_kernel(GemvParams p
     for (int v = 0; v < NI; ++v) {
 #pragma unroll
       for (int m = 0; m < NR; ++m) t[m][v] = wl(wrow[m][v] + k);
-      const f4 x = *reinterpret_cast<const f4*>(xrow[v] + k);
-      t[NR][v] = (ok && xok[v]) ? x : f4{0.f, 0.f, 0.f, 0.f};
+      if (xlive(v)) {
+        const f4 x = *reinterpret_cast<const f4*>(xrow[v] + k);
+        t[NR][v] = (ok && xok[v]) ? x : f4{0.f, 0.f, 0.f, 0.f};
+      }
     }
   };
   float* my = lds + wave * (NR + 1) * TILE;
+#pragma unroll
+  for (int v = 0; v < NI; ++v)
+    if (!xlive(v)) *reinterpret_cast<f4*>(my + NR * TILE + (RPI * v + lr) * STR + 4 * lc) = f4{0.f, 0.f, 0.f, 0.f};
   f32x4 acc[NR];
 #pragma unroll
   for (int m = 0; m < NR; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -181,7 +191,7 @@ __global__ void __launch_bounds__(kMfmaWaves * 64) gemv_mfma_kernel(GemvParams p
     for (int m = 0; m <= NR; ++m)
 #pragma unroll
       for (int v = 0; v < NI; ++v)
-        *reinterpret_cast<f4*>(my + m * TILE + (RPI * v + lr) * STR + 4 * lc) = t[m][v];
+        if (m < NR || xlive(v)) *reinterpret_cast<f4*>(my + m * TILE + (RPI * v + lr) * STR + 4 * lc) = t[m][v];
     asm volatile("" ::: "memory");  // same-wave LDS ops execute in order
 #pragma unroll
     for (int u = 0; u < U; ++u) {
