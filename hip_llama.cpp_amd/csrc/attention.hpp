@@ -215,17 +215,45 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane)
 #pragma unroll
         for (int c = 0; c < VPL; ++c) vv[u][c] = vr[c];
       }
+      const unsigned qo = (unsigned)(h * HS + (lane % LPK) * 4) * 8u;
+      const unsigned ko = (unsigned)(p.dim + kvh * HS + (lane % LPK) * 4) * 8u;
+      const unsigned vo = (unsigned)(p.dim + p.kv_dim + kvh * HS + lane * VPL) * 8u;
+      // the new key / value row: granules of this chunk when it holds position T-1
+      f4 kn = f4{0.f, 0.f, 0.f, 0.f};
+      float vn[VPL];
+#pragma unroll
+      for (int c = 0; c < VPL; ++c) vn[c] = 0.f;
+      bool kvready = false;
       if (!qready) {
-        qv = gran_wait4(rg, (unsigned)(h * HS + (lane % LPK) * 4) * 8u, w.tag_in, w.err);
+        // q, and the new k / v row if this chunk holds it, requested together: one round
+        // trip once the QKV epilogues have published (late granules are re-polled singly)
+        const v4u qa = ld16_sc1(rg, qo), qb = ld16_sc1(rg, qo + 16);
+        v4u ka = v4u{0u, 0u, 0u, 0u}, kb = ka;
+        unsigned long long vr[VPL];
+        if (t1 == T) {
+          ka = ld16_sc1(rg, ko);
+          kb = ld16_sc1(rg, ko + 16);
+#pragma unroll
+          for (int c = 0; c < VPL; ++c) vr[c] = ld8_sc1(w.gqkv + vo / 8 + c);
+        }
+        qv = gran4_ok(qa, qb, w.tag_in) ? gran4_val(qa, qb) : gran_wait4(rg, qo, w.tag_in, w.err);
         qready = true;
         if (w.ts && lane == 0) w.ts[0] = __builtin_amdgcn_s_memrealtime();
+        if (t1 == T) {
+          kn = gran4_ok(ka, kb, w.tag_in) ? gran4_val(ka, kb) : gran_wait4(rg, ko, w.tag_in, w.err);
+#pragma unroll
+          for (int c = 0; c < VPL; ++c)
+            vn[c] = (unsigned)(vr[c] >> 32) == w.tag_in ? __uint_as_float((unsigned)vr[c])
+                                                       : gran_wait(w.gqkv + vo / 8 + c, w.tag_in, w.err);
+          kvready = true;
+        }
       }
       if (t1 == T) {  // this chunk holds the new row
-        const unsigned kofs = (unsigned)(p.dim + kvh * HS), vofs = (unsigned)(p.dim + p.kv_dim + kvh * HS);
-        const f4 kn = gran_wait4(rg, (kofs + (lane % LPK) * 4) * 8u, w.tag_in, w.err);
-        float vn[VPL];
+        if (!kvready) {
+          kn = gran_wait4(rg, ko, w.tag_in, w.err);
 #pragma unroll
-        for (int c = 0; c < VPL; ++c) vn[c] = gran_wait(w.gqkv + vofs + lane * VPL + c, w.tag_in, w.err);
+          for (int c = 0; c < VPL; ++c) vn[c] = gran_wait(w.gqkv + vo / 8 + c, w.tag_in, w.err);
+        }
         if (w.ts && lane == 0) w.ts[1] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
         for (int i = 0; i < NI; ++i)
