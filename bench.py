@@ -49,7 +49,9 @@ def main():
     ap.add_argument("--splits", type=int, default=0)
     ap.add_argument("--no-persistent", action="store_true",
                     help="multi-launch step instead of the one-launch persistent step (batch 1)")
-    ap.add_argument("--cpu-baseline-tokens", type=int, default=2)
+    ap.add_argument("--cpu-baseline-tokens", type=int, default=0,
+                    help="greedy tokens the CPU baseline decodes (0: as many as fit --cpu-baseline-seconds)")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--prof-steps", type=int, default=16)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (CPU rehearsal)")
@@ -193,27 +195,32 @@ def main():
 
     # ---------------- CPU baseline: the oracle (bit-exact seq.cpp / runq.c restatement), same model
     cpu = None
-    if rank == 0 and world == 1 and not args.skip_cpu and args.cpu_baseline_tokens > 0:
+    if rank == 0 and world == 1 and not args.skip_cpu and args.cpu_baseline_tokens >= 0:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle as O
         threads = min(16, os.cpu_count() or 1)
         O.set_threads(threads)  # weight synthesis (+ int8 quantisation) only
         ref = O.Model(cfg_t, shared, seed=SEED)
-        n = args.cpu_baseline_tokens
         if q8:
             ref.build_q8(gs)
             cores = threads  # runq.c's matmul is OpenMP-parallel (runq.c:324)
-            tc = time.perf_counter()
-            ctoks = ref.q8_greedy(1, 0, n)
+            run = lambda m: ref.q8_greedy(1, 0, m)
         else:
             O.set_threads(1)
             cores = 1  # seq.cpp is single-threaded
+            run = lambda m: ref.greedy(1, 0, m)
+        n = args.cpu_baseline_tokens
+        if n <= 0:  # bounded sample: as many tokens as fit the time budget (one token calibrates)
             tc = time.perf_counter()
-            ctoks = ref.greedy(1, 0, n)
+            run(1)
+            n = max(2, min(K, S, int(args.cpu_baseline_seconds / max(time.perf_counter() - tc, 1e-6))))
+        tc = time.perf_counter()
+        ctoks = run(n)
         tcpu = time.perf_counter() - tc
         gtoks = dec.greedy([1] * B, pos0, n)[:, 0].tolist()
         cpu = {"value": round(n / tcpu, 4), "unit": "tok/s", "cores": cores, "kind": "port",
-               "sample": f"{n} greedy tokens from BOS (pos 0..{n - 1}) of the same synthetic {mname} "
+               "sample": f"{n} greedy tokens (as many as fit ~{args.cpu_baseline_seconds:g} s unless "
+                         f"--cpu-baseline-tokens) from BOS (pos 0..{n - 1}) of the same synthetic {mname} "
                          f"{args.dtype} model with oracle/oracle.c (bit-exact "
                          f"{'runq.c' if q8 else 'src/seq.cpp'} restatement), {cores} thread(s)",
                "tokens_match_gpu": ctoks == gtoks}
