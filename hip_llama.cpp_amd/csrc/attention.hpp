@@ -145,6 +145,9 @@ struct AttnWaveParams {
   unsigned tag_in, tag_out;
   unsigned* err;
   unsigned long long* ts;          // optional timeline (persistent step trace): q ready, k/v ready, done
+  // int8 weights (persistent step): the output leaves quantised instead (publish_head):
+  // {4 codes, tag} granules [dim/4] and {group scale, tag} granules [dim/64]; null: fp32 gout
+  unsigned long long *gq8, *gq8s;
 };
 
 TL_DEVICE void st_sc1(float* p, float v) { st1_sc1(p, v); }
@@ -154,8 +157,59 @@ TL_DEVICE float ld_sc1(const float* p) { return ld1_sc1(p); }
 // wave retire in order, this only stops the compiler from moving them.
 TL_DEVICE void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// The body of one attention unit, run by one full wave.  `sc` (a 64-float LDS strip) is no
-// longer used; `unit` must be wave-uniform.  Also used inside the persistent step
+// Persistent step: publish head h's output row (lane holds columns lane*VPL + c).  fp32
+// weights: one {value, tag} granule per value.  int8 weights (w.gq8 set): runq's activation
+// quantisation of the row's 64-value groups happens here (runq.c:145-171; the arithmetic of
+// the staging's q8_pack on the same floats, so the codes are the ones the Wo phase computed
+// itself before) and the row leaves as {4 codes, tag} and {scale, tag} granules: the Wo
+// phase gathers a quarter of the bytes and quantises nothing.  `strip`: the wave's LDS strip
+// (>= HS bytes).  All 64 lanes active.
+template <int HS>
+TL_DEVICE void publish_head(const AttnWaveParams& w, int h, const float* v, float* strip, int lane) {
+  constexpr int VPL = HS / 64;
+  if (!w.gq8) {
+#pragma unroll
+    for (int c = 0; c < VPL; ++c) st8_sc1(w.gout + h * HS + lane * VPL + c, gran(w.tag_out, v[c]));
+    return;
+  }
+  // group g of the head: lanes [g*64/VPL, (g+1)*64/VPL), i.e. 16-lane rows [g*RPG, (g+1)*RPG)
+  constexpr int RPG = 4 / VPL;
+  float m = 0.f;
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) m = fmaxf(m, fabsf(v[c]));
+  m = row16_max(m);
+  float sc[VPL];
+#pragma unroll
+  for (int g = 0; g < VPL; ++g) {
+    float gm = lane_f(m, 16 * g * RPG);
+#pragma unroll
+    for (int r = 1; r < RPG; ++r) gm = fmaxf(gm, lane_f(m, 16 * (g * RPG + r)));
+    sc[g] = __fdiv_rn(gm, 127.0f);
+  }
+  const int mg = (lane >> 4) / RPG;  // this lane's group
+  float scale = sc[0], lsc = sc[0];
+#pragma unroll
+  for (int g = 1; g < VPL; ++g) {
+    scale = mg == g ? sc[g] : scale;
+    lsc = lane == g ? sc[g] : lsc;
+  }
+  unsigned packed = 0;
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) packed |= (unsigned)(q8_code(v[c], scale) & 0xFF) << (8 * c);
+  // VPL codes per lane -> dwords of 4 codes through the strip
+  unsigned char* sb = reinterpret_cast<unsigned char*>(strip);
+  if constexpr (VPL == 1) sb[lane] = (unsigned char)packed;
+  else if constexpr (VPL == 2) reinterpret_cast<unsigned short*>(sb)[lane] = (unsigned short)packed;
+  else reinterpret_cast<unsigned*>(sb)[lane] = packed;
+  wave_lds_fence();
+  if (lane < HS / 4)
+    st8_sc1(w.gq8 + h * (HS / 4) + lane, gran(w.tag_out, __uint_as_float(reinterpret_cast<const unsigned*>(sb)[lane])));
+  if (lane < VPL) st8_sc1(w.gq8s + h * VPL + lane, gran(w.tag_out, lsc));
+  wave_lds_fence();  // the strip is rewritten by the next unit
+}
+
+// The body of one attention unit, run by one full wave.  `sc` (a 64-float LDS strip) is used
+// only by publish_head's int8 output; `unit` must be wave-uniform.  Also used inside the persistent step
 // kernel (persist.hip) with GR = true: q and the K/V rows at position pos come from the
 // granules the QKV phase of the same launch published (rows < pos were written by earlier
 // launches and are read from the cache), and the output is published as granules.
@@ -323,8 +377,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane)
   if (whole) {
     if constexpr (GR) {
       if (w.ts && lane == 0) w.ts[2] = __builtin_amdgcn_s_memrealtime();
-#pragma unroll
-      for (int c = 0; c < VPL; ++c) st8_sc1(w.gout + h * HS + lane * VPL + c, gran(w.tag_out, o[c]));
+      publish_head<HS>(w, h, o, sc, lane);
     } else {
 #pragma unroll
       for (int c = 0; c < VPL; ++c) out[c] = o[c];
@@ -374,8 +427,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane)
 #pragma unroll
   for (int c = 0; c < VPL; ++c) acc[c] = __fdiv_rn(acc[c], L);
   if constexpr (GR) {
-#pragma unroll
-    for (int c = 0; c < VPL; ++c) st8_sc1(w.gout + h * HS + lane * VPL + c, gran(w.tag_out, acc[c]));
+    publish_head<HS>(w, h, acc, sc, lane);
   } else {
 #pragma unroll
     for (int c = 0; c < VPL; ++c) out[c] = acc[c];

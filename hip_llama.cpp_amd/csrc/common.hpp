@@ -57,6 +57,33 @@ TL_DEVICE float wave_max_u(float v) {
   return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
 }
 
+// runq.c:145-171 activation quantisation, scalar pieces (gemv_q8.hpp q8_pack, the persistent
+// step's staging and its attention output, the thaBLAS_q8_quantize_batch op).
+TL_DEVICE int q8_round(float v) {
+  // C round(): half away from zero; NaN (all-zero group, scale 0) -> 0 like the x86 reference
+  const float r = roundf(v);
+  return r != r ? 0 : (int)r;
+}
+// q = x / scale bit-identical to the IEEE division, without one: r = RN(1/scale),
+// y = RN(x r), the exact remainder e = x - y scale (FMA), RN(y + r e) = RN(x / scale)
+// (Markstein; equal on 1.28e9 values, tools/probes/q8div.c), valid away from under/overflow:
+// scales outside [1e-30, 1e30] (an all-zero group: scale 0 -> NaN -> code 0) divide.
+TL_DEVICE bool q8_fast_scale(float scale) { return scale >= 1e-30f && scale <= 1e30f; }
+TL_DEVICE float q8_div_fast(float x, float scale, float r) {
+  const float y = __fmul_rn(x, r);
+  return __builtin_fmaf(__builtin_fmaf(-y, scale, x), r, y);
+}
+// The code: with scale = max|group| / 127, |x / scale| <= 127 (1 + 2^-23), and for |y| <= 200
+// round-half-away-from-zero is the truncation of y + copysign(pred(0.5), y) (all 2.26e9 such
+// floats: tools/probes/q8round.c).
+TL_DEVICE int q8_code_fast(float x, float scale, float r) {
+  const float y = q8_div_fast(x, scale, r);
+  return (int)__fadd_rn(y, __builtin_copysignf(0.49999997f, y));
+}
+TL_DEVICE int q8_code(float x, float scale) {
+  return q8_fast_scale(scale) ? q8_code_fast(x, scale, __fdiv_rn(1.0f, scale)) : q8_round(__fdiv_rn(x, scale));
+}
+
 // Exact int32 sum over aligned groups of N = 2, 4 or 8 lanes (every lane of a group gets
 // it): quad DPP steps, then row_half_mirror (after the quad steps the two quads of a half-row
 // each hold their sum, so the mirror pairs them).

@@ -24,26 +24,12 @@
 
 namespace tl {
 
-TL_DEVICE int q8_round(float v) {
-  // C round(): half away from zero; NaN (all-zero group, scale 0) -> 0 like the x86 reference
-  const float r = roundf(v);
-  return r != r ? 0 : (int)r;
-}
-
 typedef int q8i4 __attribute__((ext_vector_type(4)));
 
-// 16 activations (one thread's slice of a group) -> 16 int8 codes packed in a q8i4:
-// q = round(x / scale), runq.c:167, bit-identical to the IEEE division.  The division costs
-// ~10 VALU instructions and every block of the persistent step quantises the whole vector,
-// so one correctly rounded reciprocal r = RN(1/scale) per thread and, per value,
-// y = RN(x r), the exact remainder e = x - y scale (FMA) and RN(y + r e), which is RN(x / scale)
-// (Markstein's theorem; checked against the division on 1.28e9 values, tools/probes/q8div.c).
-// Scales outside [1e-30, 1e30] (an all-zero group: scale 0 -> NaN -> 0) divide.
-TL_DEVICE bool q8_fast_scale(float scale) { return scale >= 1e-30f && scale <= 1e30f; }
-TL_DEVICE float q8_div_fast(float x, float scale, float r) {
-  const float y = __fmul_rn(x, r);
-  return __builtin_fmaf(__builtin_fmaf(-y, scale, x), r, y);
-}
+// 16 (or 8) activations (one thread's slice of a group) -> int8 codes packed in dwords:
+// q = round(x / scale), runq.c:167, bit-identical to the IEEE division and C round() (the
+// division-free quotient and rounding of common.hpp q8_code_fast: the division costs ~10
+// VALU instructions and every block of the persistent step quantises the whole vector).
 template <int NF4>  // NF4 float4s -> NF4 dwords of int8 codes
 TL_DEVICE void q8_pack(const f4 (&v)[NF4], float scale, int (&packed)[NF4]) {
   float q[4 * NF4];
@@ -51,14 +37,9 @@ TL_DEVICE void q8_pack(const f4 (&v)[NF4], float scale, int (&packed)[NF4]) {
   for (int u = 0; u < NF4; ++u) { q[4 * u] = v[u].x; q[4 * u + 1] = v[u].y; q[4 * u + 2] = v[u].z; q[4 * u + 3] = v[u].w; }
   int qi[4 * NF4];
   if (q8_fast_scale(scale)) {
-    // |x / scale| <= 127 (1 + 2^-23) here, and for |y| <= 200 round-half-away-from-zero is
-    // the truncation of y + copysign(pred(0.5), y) (all 2.26e9 such floats: tools/probes/q8round.c)
     const float r = __fdiv_rn(1.0f, scale);
 #pragma unroll
-    for (int i = 0; i < 4 * NF4; ++i) {
-      const float y = q8_div_fast(q[i], scale, r);
-      qi[i] = (int)__fadd_rn(y, __builtin_copysignf(0.49999997f, y));
-    }
+    for (int i = 0; i < 4 * NF4; ++i) qi[i] = q8_code_fast(q[i], scale, r);
   } else {
 #pragma unroll
     for (int i = 0; i < 4 * NF4; ++i) qi[i] = q8_round(__fdiv_rn(q[i], scale));

@@ -415,6 +415,34 @@ template <bool Q8>
 TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, signed char* xq, float* xsc,
                      const float* rmsw, float* red, int wave, int lane, unsigned long long* ts) {
   const int n4 = d.K >> 2, pad4 = Q8 ? n4 : g.nch * PL * 64;
+  if (Q8 && d.kind == PK_WO) {
+    // the attention units published the Wo input already quantised (attention.hpp
+    // publish_head): {4 codes, tag} granules, two per 16-byte load, and {scale, tag} granules
+    const auto rq = rsrc_of(p.gxq);
+    const bool hs = threadIdx.x < d.K / 64;  // (K / 64 <= PT for every supported dim)
+    unsigned long long s0 = 0;
+    if (hs) s0 = ld8_sc1(p.gxs + threadIdx.x);  // in flight with the code loads
+    for (int j = threadIdx.x; j < d.K / 8; j += PT) {
+      v4u a = ld16_sc1(rq, (unsigned)j * 16u);
+      for (unsigned spins = 0; a.y != d.tag_in || a.w != d.tag_in; ++spins) {
+        if ((spins & 255) == 255 &&
+            (spins > kGranSpinLimit || __hip_atomic_load(as_g32(p.err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+          __hip_atomic_store(as_g32(p.err), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        a = ld16_sc1(rq, (unsigned)j * 16u);
+      }
+      *reinterpret_cast<uint2*>(xq + j * 8) = make_uint2(a.x, a.z);
+    }
+    if (hs)
+      xsc[threadIdx.x] = (unsigned)(s0 >> 32) == d.tag_in ? __uint_as_float((unsigned)s0)
+                                                          : gran_wait(p.gxs + threadIdx.x, d.tag_in, p.err);
+    if (ts && lane == 0) ts[wave == 0 ? 8 : 10] = __builtin_amdgcn_s_memrealtime();  // input gathered
+    if (ts && lane == 0 && wave == 0) ts[9] = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();
+    return;
+  }
   float sq = 0.f;
   if (!d.gin) {
     const f4* emb = reinterpret_cast<const f4*>(p.emb + (long long)p.tok[0] * p.dim);
@@ -610,6 +638,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
         aw.a.kv_mul = p.kv_mul; aw.a.seq_len = p.S; aw.a.nsplit = p.NS; aw.a.min_chunk = 16;
         aw.cnt = p.tickets + (long long)l * p.H; aw.B = 1; aw.NS = p.NS;
         aw.gqkv = p.gqkv; aw.gout = p.gxb;
+        if (Q8) { aw.gq8 = p.gxq; aw.gq8s = p.gxs; }  // the Wo input leaves quantised
         aw.tag_in = tb + 5u * l + 1; aw.tag_out = tb + 5u * l + 2; aw.err = p.err;
         aw.ts = p.trace ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots + 8 : nullptr;
         const int units = p.H * p.NS;
@@ -744,6 +773,7 @@ bool persistent_prepare(PStep& p, int ncu, const char** why) {
   if (ncu < 8) return fail("too few compute units");
   if ((long long)part_weight(ncu) * (p.V > p.hid ? p.V : p.hid) >= (1ll << 32)) return fail("grid x rows exceeds 32 bits");
   if (p.q8 && p.q8 != 64) return fail("int8 group size must be 64");
+  if (p.dim / 64 > PT) return fail("dim too large for the int8 Wo staging");
   if (5 * p.L + 1 >= 4096) return fail("too many layers for the phase tags");
   // every block must own work in every phase: a hand-off buffer may be rewritten as soon as
   // the next phase's outputs are complete, which then implies every block has staged it

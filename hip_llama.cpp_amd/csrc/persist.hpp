@@ -17,6 +17,7 @@ struct PStep {
   int* out;                 // [S] greedy tokens by position (argmax tail), may be null
   // hand-off granules {value, tag} (zero once at allocation; tags are never 0)
   unsigned long long *gx, *gxb, *ghb, *gqkv;  // [dim], [dim], [hidden], [dim + 2*kv_dim]
+  unsigned long long *gxq, *gxs;  // int8: the attention output quantised, {4 codes, tag} [dim/4], {scale, tag} [dim/64]
   unsigned* sync;           // kPSyncWords barrier shards, zeroed before every launch
   unsigned* err;            // sticky: a wait gave up (1: barrier, 2: hand-off)
   unsigned* seq;            // launch sequence (tags), advanced by the kernel

@@ -174,10 +174,7 @@ __global__ void __launch_bounds__(256) k_q8_quantize(int8_t* q, float* s, const 
     int8_t* qg = q + (long long)b * n + (long long)g * gs;
     if (tl::q8_fast_scale(scale)) {  // the hot-path quotient (q8_pack16), exercised by the op tests
       const float r = __fdiv_rn(1.0f, scale);
-      for (int i = 0; i < gs; ++i) {
-        const float y = tl::q8_div_fast(xg[i], scale, r);  // the hot-path rounding too (q8_pack)
-        qg[i] = (int8_t)(int)__fadd_rn(y, __builtin_copysignf(0.49999997f, y));
-      }
+      for (int i = 0; i < gs; ++i) qg[i] = (int8_t)tl::q8_code_fast(xg[i], scale, r);  // as q8_pack
     } else {
       for (int i = 0; i < gs; ++i) qg[i] = (int8_t)tl::q8_round(__fdiv_rn(xg[i], scale));
     }
