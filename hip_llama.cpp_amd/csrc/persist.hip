@@ -406,6 +406,51 @@ TL_DEVICE void gather(__amdgpu_buffer_rsrc_t r, unsigned tag, int n4, int pad4, 
   }
 }
 
+// int8 phase without a norm (W2: the SwiGLU output): the sweep quantises as it goes.  With
+// j = t + k PT (PT a multiple of 64) the 16 lanes of a row hold the 16 float4s of one group of
+// 64, so the group max is a DPP row max; each lane writes its 4 codes and the row's first
+// lane the scale (runq.c:145-171, the arithmetic of q8_pack).  n4 % 16 == 0; groups past K
+// up to nch whole chunks get scale 0 (the products there are 0 * 0).
+template <int NB>
+TL_DEVICE void gather_q8(__amdgpu_buffer_rsrc_t r, unsigned tag, int n4, int nch, signed char* xq, float* xsc,
+                         unsigned* err) {
+  const int t = threadIdx.x, lane = t & 63;
+  for (int k0 = 0; k0 * PT < n4; k0 += NB) {
+    v4u a[NB], b[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int j = t + (k0 + k) * PT;
+      if (j < n4) {
+        a[k] = ld16_sc1(r, (unsigned)j * 32u);
+        b[k] = ld16_sc1(r, (unsigned)j * 32u + 16u);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int j = t + (k0 + k) * PT;
+      if (j - lane >= n4) continue;  // wave-uniform: the whole wave is past the input
+      f4 v = f4{0.f, 0.f, 0.f, 0.f};
+      if (j < n4) v = gran4_ok(a[k], b[k], tag) ? gran4_val(a[k], b[k]) : gran_wait4(r, (unsigned)j * 32u, tag, err);
+      const float m = row16_max(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      const float scale = __fdiv_rn(m, 127.0f);
+      int c0, c1, c2, c3;
+      if (q8_fast_scale(scale)) {
+        const float rc = __fdiv_rn(1.0f, scale);
+        c0 = q8_code_fast(v.x, scale, rc); c1 = q8_code_fast(v.y, scale, rc);
+        c2 = q8_code_fast(v.z, scale, rc); c3 = q8_code_fast(v.w, scale, rc);
+      } else {
+        c0 = q8_round(__fdiv_rn(v.x, scale)); c1 = q8_round(__fdiv_rn(v.y, scale));
+        c2 = q8_round(__fdiv_rn(v.z, scale)); c3 = q8_round(__fdiv_rn(v.w, scale));
+      }
+      if (j < n4) {
+        *reinterpret_cast<int*>(xq + 4 * j) = (c0 & 0xFF) | ((c1 & 0xFF) << 8) | ((c2 & 0xFF) << 16) | ((c3 & 0xFF) << 24);
+        if ((lane & 15) == 0) xsc[j >> 4] = scale;
+      }
+    }
+  }
+  for (int gi = n4 / 16 + t; gi < nch * 64; gi += PT) xsc[gi] = 0.f;
+}
+
 // Every wave stages the phase input into LDS (zero-padded to whole chunks), RMSNorm'd when
 // the phase has a norm (its weights were preloaded into LDS `rmsw` by the control wave).
 // The input is the previous phase's granules (all issued at once, then re-polled until
@@ -438,6 +483,13 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, sign
     if (hs)
       xsc[threadIdx.x] = (unsigned)(s0 >> 32) == d.tag_in ? __uint_as_float((unsigned)s0)
                                                           : gran_wait(p.gxs + threadIdx.x, d.tag_in, p.err);
+    if (ts && lane == 0) ts[wave == 0 ? 8 : 10] = __builtin_amdgcn_s_memrealtime();  // input gathered
+    if (ts && lane == 0 && wave == 0) ts[9] = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();
+    return;
+  }
+  if (Q8 && !d.rms && d.gin) {  // W2: quantised while it is gathered
+    gather_q8<SB>(rsrc_of(d.gin), d.tag_in, n4, g.nch, xq, xsc, p.err);
     if (ts && lane == 0) ts[wave == 0 ? 8 : 10] = __builtin_amdgcn_s_memrealtime();  // input gathered
     if (ts && lane == 0 && wave == 0) ts[9] = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
