@@ -114,6 +114,11 @@ def main():
         rel = lambda k: float(np.median((a[:, :, k] - a[:, :, 0])[live]))
         print(f"attention units ({int(live.sum() / len(att))} per layer): q {rel(8):.2f}  kv {rel(9):.2f}  "
               f"computed {rel(10):.2f}  done {rel(3):.2f} us after phase start")
+    # epilogue (all slots reduced -> epilogue issued), median and max over blocks
+    print("epilogue us (median / max over blocks): " + "  ".join(
+        f"{kind} {np.median([np.median(t[:, ph, 3] - t[:, ph, 2]) for ph in range(k, nph - 1, 5)]):.2f}/"
+        f"{np.mean([np.max(t[:, ph, 3] - t[:, ph, 2]) for ph in range(k, nph - 1, 5)]):.2f}"
+        for kind, k in (("qkv", 0), ("wo", 2), ("ffn_up", 3), ("ffn_down", 4))))
     if args.json:
         with open(args.json, "w") as f:
             json.dump(out, f, indent=1)
