@@ -379,19 +379,22 @@ TL_DEVICE void run_gemv(const PDesc& d, const PGeo& g, const PStep& p, int sw, i
 
 // Granule sweep of the phase input into the LDS strip by threads t, t + T, ...: batches of NB
 // float4 (2*NB loads in flight per thread), then re-poll what was late.  sq: sum of squares.
-template <int NB>
+// UNC: unconditional (clamped) loads, so loads issued by `mid` after them keep the compiler's
+// vmcnt waits exact (int8, where mid issues slots); otherwise only threads with input load.
+template <int NB, bool UNC, class F>
 TL_DEVICE void gather(__amdgpu_buffer_rsrc_t r, unsigned tag, int n4, int pad4, int t, int T, f4* xs, float& sq,
-                      unsigned* err) {
+                      unsigned* err, F&& mid) {
   for (int k0 = 0; k0 * T < pad4; k0 += NB) {
     v4u a[NB], b[NB];
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
-      const int j = t + (k0 + k) * T;
-      if (j < n4) {
-        a[k] = ld16_sc1(r, (unsigned)j * 32u);
-        b[k] = ld16_sc1(r, (unsigned)j * 32u + 16u);
+      const int j = t + (k0 + k) * T, jc = j < n4 ? j : n4 - 1;
+      if (UNC || j < n4) {
+        a[k] = ld16_sc1(r, (unsigned)jc * 32u);
+        b[k] = ld16_sc1(r, (unsigned)jc * 32u + 16u);
       }
     }
+    if ((k0 + NB) * T >= pad4) mid();  // after the sweep's last loads
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
       const int j = t + (k0 + k) * T;
@@ -411,20 +414,19 @@ TL_DEVICE void gather(__amdgpu_buffer_rsrc_t r, unsigned tag, int n4, int pad4, 
 // 64, so the group max is a DPP row max; each lane writes its 4 codes and the row's first
 // lane the scale (runq.c:145-171, the arithmetic of q8_pack).  n4 % 16 == 0; groups past K
 // up to nch whole chunks get scale 0 (the products there are 0 * 0).
-template <int NB>
+template <int NB, class F>
 TL_DEVICE void gather_q8(__amdgpu_buffer_rsrc_t r, unsigned tag, int n4, int nch, signed char* xq, float* xsc,
-                         unsigned* err) {
+                         unsigned* err, F&& mid) {
   const int t = threadIdx.x, lane = t & 63;
   for (int k0 = 0; k0 * PT < n4; k0 += NB) {
     v4u a[NB], b[NB];
 #pragma unroll
-    for (int k = 0; k < NB; ++k) {
-      const int j = t + (k0 + k) * PT;
-      if (j < n4) {
-        a[k] = ld16_sc1(r, (unsigned)j * 32u);
-        b[k] = ld16_sc1(r, (unsigned)j * 32u + 16u);
-      }
+    for (int k = 0; k < NB; ++k) {  // unconditional (clamped) loads: exact vmcnt bookkeeping
+      const int j = t + (k0 + k) * PT, jc = j < n4 ? j : n4 - 1;
+      a[k] = ld16_sc1(r, (unsigned)jc * 32u);
+      b[k] = ld16_sc1(r, (unsigned)jc * 32u + 16u);
     }
+    if ((k0 + NB) * PT >= n4) mid();  // after the sweep's last loads
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
       const int j = t + (k0 + k) * PT;
@@ -456,13 +458,14 @@ TL_DEVICE void gather_q8(__amdgpu_buffer_rsrc_t r, unsigned tag, int n4, int nch
 // The input is the previous phase's granules (all issued at once, then re-polled until
 // their tags match), or — QKV at layer 0, or the classifier of a model without layers —
 // the token's embedding row (weights: plain loads).  Ends with a workgroup barrier.
-template <bool Q8>
+template <bool Q8, class F>
 TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, signed char* xq, float* xsc,
-                     const float* rmsw, float* red, int wave, int lane, unsigned long long* ts) {
+                     const float* rmsw, float* red, int wave, int lane, unsigned long long* ts, F&& mid) {
   const int n4 = d.K >> 2, pad4 = Q8 ? n4 : g.nch * PL * 64;
   if (Q8 && d.kind == PK_WO) {
     // the attention units published the Wo input already quantised (attention.hpp
     // publish_head): {4 codes, tag} granules, two per 16-byte load, and {scale, tag} granules
+    mid();
     const auto rq = rsrc_of(p.gxq);
     const bool hs = threadIdx.x < d.K / 64;  // (K / 64 <= PT for every supported dim)
     unsigned long long s0 = 0;
@@ -489,7 +492,7 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, sign
     return;
   }
   if (Q8 && !d.rms && d.gin) {  // W2: quantised while it is gathered
-    gather_q8<SB>(rsrc_of(d.gin), d.tag_in, n4, g.nch, xq, xsc, p.err);
+    gather_q8<SB>(rsrc_of(d.gin), d.tag_in, n4, g.nch, xq, xsc, p.err, mid);
     if (ts && lane == 0) ts[wave == 0 ? 8 : 10] = __builtin_amdgcn_s_memrealtime();  // input gathered
     if (ts && lane == 0 && wave == 0) ts[9] = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
@@ -497,6 +500,7 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, sign
   }
   float sq = 0.f;
   if (!d.gin) {
+    mid();
     const f4* emb = reinterpret_cast<const f4*>(p.emb + (long long)p.tok[0] * p.dim);
     for (int j = threadIdx.x; j < pad4; j += PT) {
       const f4 v = j < n4 ? emb[j] : f4{0.f, 0.f, 0.f, 0.f};
@@ -506,7 +510,7 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, sign
   } else {
     // every wave sweeps (the control wave alone, 16-24 loads in flight, was 1.4x slower per
     // step: the sweep is bound by loads in flight, not by the streaming waves' queued slots)
-    gather<SB>(rsrc_of(d.gin), d.tag_in, n4, pad4, threadIdx.x, PT, xs, sq, p.err);
+    gather<SB, Q8>(rsrc_of(d.gin), d.tag_in, n4, pad4, threadIdx.x, PT, xs, sq, p.err, mid);
   }
   if (ts && lane == 0) ts[wave == 0 ? 8 : 10] = __builtin_amdgcn_s_memrealtime();  // input gathered
   float ss = 1.f;
@@ -701,7 +705,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
       const PDesc d = make_desc<Q8>(p, kind, l, tb);
       const PGeo g = geo<Q8>(d);
       stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, wave, lane,
-                p.trace ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots : nullptr);
+                p.trace ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots : nullptr, [] {});
       TRACE(1);
       float2 cs0 = make_float2(1.f, 0.f);
       if (kind == PK_QKV) {
@@ -734,15 +738,20 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
       const PDesc d = make_desc<Q8>(p, kind, kind == PK_CLS ? p.L : l, tb);
       const PGeo g = geo<Q8>(d);
       const bool tr = p.trace && sw == 0;
-      stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, wave, lane,
-                tr ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots : nullptr);
-      if (tr) TRACE(4);
-      if (ph > 0) {  // the buffers not prefetched across the phase boundary (issuing them after
-                     // the first slot's consume instead lost 2.5% int8)
+      // The buffers not prefetched across the boundary (pfn) are issued inside the staging,
+      // right after this wave's last granule loads: their data returns behind the granules
+      // (a wave's loads return in order) and the issue overlaps the sweep (issued after the
+      // staging they delayed the first slot ~2 us, after the first slot's consume -2.5%).
+      // Every load around them is unconditional, so the compiler's vmcnt waits for the
+      // granules do not cover them (with a conditional issue they did: -18%); whole slots,
+      // zero-size past the phase's end (at phase 0 this re-issues the initial prefetch).
+      auto mid = [&] {
 #pragma unroll
-        for (int i = pfn<Q8>(); i < NBUF; ++i)
-          if (sw + i * NSW < g.nslot) load_any<Q8>(d, g, p, sw + i * NSW, lane, buf[i], sc[i]);
-      }
+        for (int i = pfn<Q8>(); i < NBUF; ++i) load_any<Q8>(d, g, p, sw + i * NSW, lane, buf[i], sc[i]);
+      };
+      stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, wave, lane,
+                tr ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots : nullptr, mid);
+      if (tr) TRACE(4);
       run_gemv<Q8>(d, g, p, sw, lane, xs, xq, xsc, res, buf, sc, ctr,
                    tr ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots + 5 : nullptr);
       if (tr) TRACE(6);
