@@ -23,7 +23,13 @@ namespace tl {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kMfmaWaves = 4;
+#ifndef MFMA_WAVES
+#define MFMA_WAVES 4
+#endif
+#ifndef MFMA_U
+#define MFMA_U 4
+#endif
+constexpr int kMfmaWaves = MFMA_WAVES;
 
 // One output of the decode epilogues (gemv.hpp epilogue) for row/item `item`, sequence b.
 template <int MODE>
@@ -106,7 +112,7 @@ __global__ void __launch_bounds__(kMfmaWaves * 64) gemv_mfma_kernel(GemvParams p
   constexpr int W = kMfmaWaves;
   constexpr bool TWO = MODE == GM_SWIGLU;
   constexpr int NR = TWO ? 2 : 1;      // weight tiles per group; tile NR is the activations
-  constexpr int U = 4;                 // 16-k steps per group
+  constexpr int U = MFMA_U;            // 16-k steps per group
   constexpr int LPR = U * 4;           // lanes per row in a load (16 B each): 256-B runs
   constexpr int RPI = 64 / LPR;        // rows per load instruction
   constexpr int NI = 16 / RPI;         // load instructions per 16-row tile
