@@ -591,6 +591,11 @@ static int enqueue_persistent(thallama_decoder* d, bool argmax) {
 
 // After a synchronisation: did a persistent grid barrier give up?  (Only possible if the
 // grid was not co-resident; the step's results are then wrong and the path is disabled.)
+// check_persist's status when a persistent launch gave up (its outputs are garbage) and the
+// path is now disabled: the public entry points then re-run the call on the multi-launch path
+// (every K/V row the failed call wrote is rewritten, in order, before it is read again).
+constexpr int kPersistFellBack = (int)hipErrorLaunchFailure;
+
 static int check_persist(thallama_decoder* d) {
   if (!d->psync) return 0;
   unsigned err = 0;
@@ -600,8 +605,12 @@ static int check_persist(thallama_decoder* d) {
   TL_TRY(hipMemset(d->cnt_d, 0, sizeof(unsigned) * (size_t)d->B * d->H));
   d->pok = false;
   d->pwhy = "a grid barrier timed out";
+  if (d->exec) {  // the captured graph holds the persistent launch
+    (void)hipGraphExecDestroy(d->exec);
+    d->exec = nullptr;
+  }
   g_last_error = "persistent step: a grid barrier timed out (grid not co-resident); path disabled";
-  return (int)hipErrorLaunchFailure;
+  return kPersistFellBack;
 }
 
 extern "C" int thallama_decoder_persistent(thallama_decoder* d) { return d && use_persist(d) ? 1 : 0; }
@@ -650,7 +659,16 @@ static int upload_tok_pos(thallama_decoder* d, const int* token_h, const int* po
   return 0;
 }
 
+static int decoder_forward_once(thallama_decoder* d, const int* token_h, const int* pos_h, float* logits_h);
+
 extern "C" int thallama_decoder_forward(thallama_decoder* d, const int* token_h, const int* pos_h, float* logits_h) {
+  const bool persistent = d && use_persist(d);
+  int r = decoder_forward_once(d, token_h, pos_h, logits_h);
+  if (r == kPersistFellBack && persistent && !use_persist(d)) r = decoder_forward_once(d, token_h, pos_h, logits_h);
+  return r;
+}
+
+static int decoder_forward_once(thallama_decoder* d, const int* token_h, const int* pos_h, float* logits_h) {
   if (!d || !token_h || !pos_h) return (int)hipErrorInvalidValue;
   int r = upload_tok_pos(d, token_h, pos_h);
   if (r) return r;
@@ -664,8 +682,20 @@ extern "C" int thallama_decoder_forward(thallama_decoder* d, const int* token_h,
   return check_persist(d);
 }
 
+static int decoder_greedy_once(thallama_decoder* d, const int* token0_h, const int* pos0_h, int n_steps,
+                               int* tokens_out_h, int sync);
+
 extern "C" int thallama_decoder_greedy(thallama_decoder* d, const int* token0_h, const int* pos0_h, int n_steps,
                                        int* tokens_out_h, int sync) {
+  const bool persistent = d && use_persist(d);
+  int r = decoder_greedy_once(d, token0_h, pos0_h, n_steps, tokens_out_h, sync);
+  if (r == kPersistFellBack && persistent && !use_persist(d))
+    r = decoder_greedy_once(d, token0_h, pos0_h, n_steps, tokens_out_h, sync);
+  return r;
+}
+
+static int decoder_greedy_once(thallama_decoder* d, const int* token0_h, const int* pos0_h, int n_steps,
+                               int* tokens_out_h, int sync) {
   if (!d || !token0_h || !pos0_h || n_steps < 0) return (int)hipErrorInvalidValue;
   for (int b = 0; b < d->B; ++b)
     if (pos0_h[b] + n_steps > d->S) {
