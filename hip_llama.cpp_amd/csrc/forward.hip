@@ -137,6 +137,7 @@ struct thallama_decoder {
   bool use_graph = false;
   bool profile = false;
   bool persist = true;          // requested (THALLAMA_OPT_PERSISTENT)
+  bool pfault = false;          // test hook: the next persistent launch loses block 0
   hipGraphExec_t exec = nullptr;
   // persistent one-launch step (persist.hip)
   int ncu = 0;
@@ -339,6 +340,10 @@ extern "C" int thallama_decoder_set(thallama_decoder* d, int key, int value) {
     case THALLAMA_OPT_USE_GRAPH: d->use_graph = value != 0; break;
     case THALLAMA_OPT_PROFILE: d->profile = value != 0; break;
     case THALLAMA_OPT_PERSISTENT: d->persist = value != 0; break;
+    case THALLAMA_OPT_PERSIST_FAULT:
+      d->pfault = value != 0;
+      if (d->exec) { (void)hipGraphExecDestroy(d->exec); d->exec = nullptr; }
+      break;
     default: return (int)hipErrorInvalidValue;
   }
   if (d->exec) {  // options are baked into a captured graph: recapture on next use
@@ -568,6 +573,8 @@ static int enqueue_persistent(thallama_decoder* d, bool argmax) {
   p.err = d->psync + d->psync_zero; p.seq = p.err + 1; p.bmax = d->pbmax;
   p.argmax = argmax ? 1 : 0;
   p.trace = d->ptrace;
+  p.fault = d->pfault ? 1 : 0;
+  d->pfault = false;  // one-shot (a captured graph keeps it; the give-up drops the graph)
   if (d->q8) {
     p.q8 = d->w8.group_size;
     for (int t = 0; t < 7; ++t) {

@@ -798,6 +798,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
 
 template <int HS, bool Q8>
 __global__ void __launch_bounds__(PT) persistent_step_kernel(PStep p) {
+  if (p.fault && blockIdx.x == 0) return;  // test hook: a missing block (every wait is bounded)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* strips = reinterpret_cast<float*>(smem);  // 64: attention score strip of wave 0
   float* xres = strips + 64;                        // kPResidFloats: residual slice

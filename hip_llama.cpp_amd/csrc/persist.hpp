@@ -37,6 +37,8 @@ struct PStep {
   const signed char* qcls;
   const float* scls;
   int q8_pad;               // LDS bytes of the quantised activation strip (Q8 only)
+  int fault;                // test hook (THALLAMA_OPT_PERSIST_FAULT): block 0 exits at once, as
+                            // if the grid were not co-resident; every other wait gives up
 };
 
 constexpr int kPSyncWords = 8 * 32;   // 8 shard counters, one 128-B line each

@@ -91,7 +91,7 @@ STATUS = {0: "SUCCESS", 1: "NOT_INITIALIZED", 2: "ALLOC_FAILED", 3: "INVALID_VAL
 # kernel classes (include/thallama.h)
 K_QKV, K_ATTN, K_WO, K_FFN_UP, K_FFN_DOWN, K_CLS, K_ARGMAX, K_STEP = range(8)
 K_NAMES = ["qkv", "attn", "wo", "ffn_up", "ffn_down", "cls", "argmax", "step"]
-OPT_NT_WEIGHTS, OPT_ATTN_SPLITS, OPT_USE_GRAPH, OPT_PROFILE, OPT_PERSISTENT = 1, 2, 3, 4, 5
+OPT_NT_WEIGHTS, OPT_ATTN_SPLITS, OPT_USE_GRAPH, OPT_PROFILE, OPT_PERSISTENT, OPT_PERSIST_FAULT = 1, 2, 3, 4, 5, 6
 
 _lib = None
 

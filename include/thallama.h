@@ -35,6 +35,10 @@ enum {
   THALLAMA_OPT_PERSISTENT = 5,   /* 0/1: whole step as ONE persistent launch (batch 1, fp32,
                                     head size 64/128; default 1 where supported).  Profiled
                                     as the single class THALLAMA_K_STEP. */
+  THALLAMA_OPT_PERSIST_FAULT = 6,  /* test hook: the next persistent launch runs without its
+                                    block 0 (as if the grid were not co-resident): its waits
+                                    give up, the call disables the path and re-runs on the
+                                    multi-launch step. */
 };
 
 /* 1 if the decoder runs its steps as one persistent launch (THALLAMA_OPT_PERSISTENT

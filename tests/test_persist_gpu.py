@@ -65,6 +65,21 @@ def test_greedy_matches_oracle(gpu, oracle, cfg, shared, graph):
     assert_ref_close(dec.logits()[0], last, 1e-4, "last-step logits")
 
 
+@pytest.mark.parametrize("graph", [0, 1])
+def test_give_up_falls_back(gpu, oracle, graph):
+    """A persistent launch whose grid is not co-resident (simulated: block 0 missing) must not
+    hang or return garbage: its bounded waits give up, the call disables the path and re-runs
+    on the multi-launch step, and the tokens still equal the oracle's."""
+    _, _, _, dec = decoder(gpu, SMALL, 0, 42, 1)
+    dec.set(gpu.OPT_USE_GRAPH, graph)
+    want = oracle.Model(SMALL, 0, seed=42).greedy(1, 0, 12)
+    assert dec.greedy([1], [0], 4)[:, 0].tolist() == want[:4]
+    assert dec.persistent()
+    dec.set(gpu.OPT_PERSIST_FAULT, 1)
+    assert dec.greedy([want[3]], [4], 8)[:, 0].tolist() == want[4:12]
+    assert not dec.persistent()
+
+
 @pytest.mark.parametrize("cfg", [SMALL, HEAD128, RAGGED])
 def test_forced_logits_every_step(gpu, oracle, cfg):
     _, _, _, dec = decoder(gpu, cfg, 0, 9, 1)
