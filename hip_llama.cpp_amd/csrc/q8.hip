@@ -9,11 +9,21 @@
 #include "../../include/thaQ8.hpp"
 #include "../../include/hip_helper.hpp"
 #include "gemv_q8.hpp"
+#include "gemv_q8_mfma.hpp"
 #include "q8_dispatch.hpp"
 
 namespace tl {
 
 static inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// The int8 matrix-core GEMV for 4..8 sequences (env THALLAMA_Q8_MFMA=0 turns it off).
+static bool q8_mfma_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("THALLAMA_Q8_MFMA");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
 
 bool gemv_q8_fast_ok(const GemvParams& p) {
   if (p.K <= 0 || p.gs < 32 || p.gs > 128 || (p.gs & (p.gs - 1)) || p.K % p.gs || (p.K & 15)) return false;
@@ -136,7 +146,20 @@ static hipError_t launch_q8_mode(const GemvParams& p0, hipStream_t s, bool nt) {
     } else {
       p.xq = nullptr;
     }
-    if (p.nb == 1) launch_q8_nb<MODE, 1>(p, s, nt);
+    if (p.nb >= 4 && p.xq && p.gs == 64 && (p.K & 255) == 0 && q8_mfma_enabled()) {
+      // 4..8 sequences: the int8 matrix-core kernel (gemv_q8_mfma.hpp), K split across blocks
+      // like the fp32 one (in 256-byte runs)
+      const int rows = MODE == GM_QKV ? 2 * p.n_items : p.n_items;
+      const int tiles = (rows + 15) / 16, nruns = p.K >> 8;
+      int ms = p.mpart && p.mcnt ? mfma_target_blocks() / tiles : 1;
+      const int cap = nruns / kMfmaWaves;
+      if (ms > cap) ms = cap;
+      if (ms < 1) ms = 1;
+      p.msteps = (nruns + ms - 1) / ms;
+      p.msplit = (nruns + p.msteps - 1) / p.msteps;
+      if (nt) hipLaunchKernelGGL((gemv_q8_mfma_kernel<MODE, true>), dim3(tiles * p.msplit), dim3(kMfmaWaves * 64), 0, s, p);
+      else hipLaunchKernelGGL((gemv_q8_mfma_kernel<MODE, false>), dim3(tiles * p.msplit), dim3(kMfmaWaves * 64), 0, s, p);
+    } else if (p.nb == 1) launch_q8_nb<MODE, 1>(p, s, nt);
     else if (p.nb == 2) launch_q8_nb<MODE, 2>(p, s, nt);
     else if (p.nb <= 4) launch_q8_nb<MODE, 4>(p, s, nt);
     else launch_q8_nb<MODE, 8>(p, s, nt);

@@ -144,6 +144,33 @@ def test_q8_drift_is_bounded(gpu, oracle):
         assert int(np.argmax(got)) == int(np.argmax(want)) or abs(float(np.sort(want)[-1] - np.sort(want)[-2])) < Q8_TOL
 
 
+@pytest.mark.parametrize("cfg,B", [(SMALL_GQA, 4), (SMALL_GQA, 8), ((768, 2048, 2, 12, 12, 4096, 256), 5)])
+def test_q8_batched_decoder_matches_runq(gpu, oracle, cfg, B):
+    """4..8 sequences take the int8 matrix-core GEMV (gemv_q8_mfma.hpp): exact int32 group dots
+    by v_mfma_i32_16x16x64_i8, scaled per group in fp32.  Teacher-forced logits of every sequence
+    (own tokens, own positions) against runq's forward, within Q8_TOL."""
+    c = gpu.Config.make(*cfg)
+    q = gpu.DeviceModelQ8(c, 0, 64, from_model=gpu.DeviceModel(c, 0, seed=11))
+    dec = gpu.Decoder(q, gpu.DeviceState(c, B))
+    refs = []
+    for _ in range(B):
+        r = oracle.Model(cfg, 0, seed=11)
+        r.build_q8(64)
+        refs.append(r)
+    rng_ = np.random.default_rng(B)
+    toks = rng_.integers(0, cfg[5], (B, 5))
+    off = rng_.integers(0, 3, B)  # sequence b starts at position off[b]
+    for b in range(B):  # prefix: token toks[b, 0] at positions 0 .. off[b]-1
+        for p in range(off[b]):
+            refs[b].q8_forward(int(toks[b, 0]), p)
+    for p in range(int(off.max())):  # (a sequence past its prefix rewrites position off[b], as step 0 will)
+        dec.forward([int(t) for t in toks[:, 0]], [int(min(p, o)) for o in off])
+    for i in range(5):
+        got = dec.forward(toks[:, i].tolist(), (off + i).tolist())
+        for b in range(B):
+            assert_ref_close(got[b], refs[b].q8_forward(int(toks[b, i]), int(off[b] + i)), Q8_TOL, f"b{b} step {i}")
+
+
 def test_q8_forward_batch_c_abi(gpu, oracle):
     cfg = SMALL_GQA
     c = gpu.Config.make(*cfg)
