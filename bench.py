@@ -257,7 +257,8 @@ def main():
                     "frac": round(ffn["GBps"] / HBM_PEAK_GBS, 4),
                     "traffic": None if q8 else traffic_of("void tl::gemv_kernel<2, 1, 1, true, 4, false>"),
                     "traffic_source": f"profiles/{pmc_file} (rocprofv3 --pmc)",
-                    "kernel": ("gemv_q8_kernel" if q8 else "gemv_kernel") + "<GM_SWIGLU> (RMSNorm + W1/W3 + SwiGLU)",
+                    "kernel": ("gemv_q8" if q8 else "gemv") + ("_mfma" if B >= 4 else "") + "_kernel<GM_SWIGLU> "
+                              "(RMSNorm + W1/W3 + SwiGLU" + (", matrix cores)" if B >= 4 else ")"),
                     "bytes_per_launch": launch_bytes(tl.K_FFN_UP, [0] * B), "avg_us": round(ffn["avg_us"], 2)}
         out = {
             "metric": "decode tokens/sec (greedy, whole model) + achieved HBM GB/s fraction",
