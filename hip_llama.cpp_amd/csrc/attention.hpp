@@ -148,6 +148,10 @@ struct AttnWaveParams {
   // int8 weights (persistent step): the output leaves quantised instead (publish_head):
   // {4 codes, tag} granules [dim/4] and {group scale, tag} granules [dim/64]; null: fp32 gout
   unsigned long long *gq8, *gq8s;
+  // int8 weights, multi-launch batched step: the output row is also stored quantised (codes
+  // [b][dim], group scales [b][dim/64]) so the Wo launch that follows needs no quantise pass
+  signed char* xq8;
+  float* xq8s;
 };
 
 TL_DEVICE void st_sc1(float* p, float v) { st1_sc1(p, v); }
@@ -156,6 +160,59 @@ TL_DEVICE float ld_sc1(const float* p) { return ld1_sc1(p); }
 // Orders one wave's LDS strip writes before its reads (and vice versa): LDS ops of a
 // wave retire in order, this only stops the compiler from moving them.
 TL_DEVICE void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// runq's activation quantisation of one head's output row (lane holds columns lane*VPL + c)
+// over its 64-value groups: returns this lane's VPL codes packed low byte first; lane g < VPL
+// gets group g's scale in `lsc`.  All 64 lanes active.
+template <int HS>
+TL_DEVICE unsigned head_q8(const float* v, int lane, float& lsc) {
+  constexpr int VPL = HS / 64;
+  // group g of the head: lanes [g*64/VPL, (g+1)*64/VPL), i.e. 16-lane rows [g*RPG, (g+1)*RPG)
+  constexpr int RPG = 4 / VPL;
+  float m = 0.f;
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) m = fmaxf(m, fabsf(v[c]));
+  m = row16_max(m);
+  float sc[VPL];
+#pragma unroll
+  for (int g = 0; g < VPL; ++g) {
+    float gm = lane_f(m, 16 * g * RPG);
+#pragma unroll
+    for (int r = 1; r < RPG; ++r) gm = fmaxf(gm, lane_f(m, 16 * (g * RPG + r)));
+    sc[g] = __fdiv_rn(gm, 127.0f);
+  }
+  const int mg = (lane >> 4) / RPG;  // this lane's group
+  float scale = sc[0];
+  lsc = sc[0];
+#pragma unroll
+  for (int g = 1; g < VPL; ++g) {
+    scale = mg == g ? sc[g] : scale;
+    lsc = lane == g ? sc[g] : lsc;
+  }
+  unsigned packed = 0;
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) packed |= (unsigned)(q8_code(v[c], scale) & 0xFF) << (8 * c);
+  return packed;
+}
+
+// Multi-launch step: store head h of sequence b (fp32 row, and the int8 codes + group scales
+// when w.xq8 is set).
+template <int HS>
+TL_DEVICE void store_head(const AttnWaveParams& w, int b, int h, const float* v, int lane) {
+  constexpr int VPL = HS / 64;
+  const AttnParams& p = w.a;
+  float* out = p.out + (long long)b * p.dim + h * HS + lane * VPL;
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) out[c] = v[c];
+  if (!w.xq8) return;
+  float lsc;
+  const unsigned packed = head_q8<HS>(v, lane, lsc);
+  signed char* q = w.xq8 + (long long)b * p.dim + h * HS + lane * VPL;
+  if constexpr (VPL == 1) *q = (signed char)packed;
+  else if constexpr (VPL == 2) *reinterpret_cast<unsigned short*>(q) = (unsigned short)packed;
+  else *reinterpret_cast<unsigned*>(q) = packed;
+  if (lane < VPL) w.xq8s[(long long)b * (p.dim / 64) + h * VPL + lane] = lsc;
+}
 
 // Persistent step: publish head h's output row (lane holds columns lane*VPL + c).  fp32
 // weights: one {value, tag} granule per value.  int8 weights (w.gq8 set): runq's activation
@@ -172,30 +229,8 @@ TL_DEVICE void publish_head(const AttnWaveParams& w, int h, const float* v, floa
     for (int c = 0; c < VPL; ++c) st8_sc1(w.gout + h * HS + lane * VPL + c, gran(w.tag_out, v[c]));
     return;
   }
-  // group g of the head: lanes [g*64/VPL, (g+1)*64/VPL), i.e. 16-lane rows [g*RPG, (g+1)*RPG)
-  constexpr int RPG = 4 / VPL;
-  float m = 0.f;
-#pragma unroll
-  for (int c = 0; c < VPL; ++c) m = fmaxf(m, fabsf(v[c]));
-  m = row16_max(m);
-  float sc[VPL];
-#pragma unroll
-  for (int g = 0; g < VPL; ++g) {
-    float gm = lane_f(m, 16 * g * RPG);
-#pragma unroll
-    for (int r = 1; r < RPG; ++r) gm = fmaxf(gm, lane_f(m, 16 * (g * RPG + r)));
-    sc[g] = __fdiv_rn(gm, 127.0f);
-  }
-  const int mg = (lane >> 4) / RPG;  // this lane's group
-  float scale = sc[0], lsc = sc[0];
-#pragma unroll
-  for (int g = 1; g < VPL; ++g) {
-    scale = mg == g ? sc[g] : scale;
-    lsc = lane == g ? sc[g] : lsc;
-  }
-  unsigned packed = 0;
-#pragma unroll
-  for (int c = 0; c < VPL; ++c) packed |= (unsigned)(q8_code(v[c], scale) & 0xFF) << (8 * c);
+  float lsc;
+  const unsigned packed = head_q8<HS>(v, lane, lsc);
   // VPL codes per lane -> dwords of 4 codes through the strip
   unsigned char* sb = reinterpret_cast<unsigned char*>(strip);
   if constexpr (VPL == 1) sb[lane] = (unsigned char)packed;
@@ -373,14 +408,12 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane)
     }
   }
 
-  float* out = p.out + (long long)b * p.dim + h * HS + lane * VPL;
   if (whole) {
     if constexpr (GR) {
       if (w.ts && lane == 0) w.ts[2] = __builtin_amdgcn_s_memrealtime();
       publish_head<HS>(w, h, o, sc, lane);
     } else {
-#pragma unroll
-      for (int c = 0; c < VPL; ++c) out[c] = o[c];
+      store_head<HS>(w, b, h, o, lane);
     }
     return;
   }
@@ -429,8 +462,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane)
   if constexpr (GR) {
     publish_head<HS>(w, h, acc, sc, lane);
   } else {
-#pragma unroll
-    for (int c = 0; c < VPL; ++c) out[c] = acc[c];
+    store_head<HS>(w, b, h, acc, lane);
   }
   if (lane == 0) __hip_atomic_store(w.cnt + bh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -377,6 +377,14 @@ static hipError_t gemv(thallama_decoder* d, int mode, tl::GemvParams& p, const Q
 }
 #define Q8L(name) (d->q8 ? &d->w8.name[l] : nullptr)
 
+// int8 decoder, 2..8 sequences, wave-level attention, runq groups of 64: attention stores its
+// output row quantised as well (attention.hpp: store_head), the codes Wo's quantise pass would
+// have produced from the same floats, so that pass is skipped
+static int q8_attn_quant(const thallama_decoder* d) {
+  return d->q8 && d->xq_d && d->B >= 2 && d->B <= 8 && d->w8.group_size == 64 &&
+         (d->hs == 64 || d->hs == 128 || d->hs == 256) && (d->dim % 64) == 0;
+}
+
 // Enqueue one decode step reading tok_d / pos_d; logits land in s.logits.
 static int enqueue_step(thallama_decoder* d) {
   const int dim = d->dim, hid = d->hidden, kvd = d->kv_dim, S = d->S;
@@ -449,6 +457,10 @@ static int enqueue_step(thallama_decoder* d) {
         const int max_chunks = (S + kAttnChunk - 1) / kAttnChunk;
         wp.NS = d->nsplit < max_chunks ? d->nsplit : max_chunks;
         const int units = d->B * d->H * wp.NS;
+        if (q8_attn_quant(d)) {
+          wp.xq8 = d->xq_d;
+          wp.xq8s = d->xqs_d;
+        }
         if (d->hs == 64)
           hipLaunchKernelGGL((tl::attn_wave_kernel<64, kAttnChunk>), dim3(units), dim3(64), 0, d->stream, wp);
         else if (d->hs == 128)
@@ -489,6 +501,7 @@ static int enqueue_step(thallama_decoder* d) {
       p.x_stride = dim;
       p.y = s.x;
       p.y_stride = dim;
+      p.xq_ready = q8_attn_quant(d);
       int ev = prof_begin(d);
       TL_TRY(gemv(d, tl::GM_RESID, p, Q8L(wo), nullptr, nullptr));
       prof_end(d, THALLAMA_K_WO, ev);

@@ -72,6 +72,7 @@ struct GemvParams {
   // once per block
   signed char* xq;
   float* xqs;
+  int xq_ready;  // xq/xqs already hold this launch's quantised activations (attention wrote them)
   // optional split-K scratch for the matrix-core path: per-block partial tiles
   // [tiles][splits][2][256] and one ticket per tile (zero between launches)
   float* mpart;

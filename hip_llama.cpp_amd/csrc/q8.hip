@@ -137,7 +137,9 @@ static hipError_t launch_q8_mode(const GemvParams& p0, hipStream_t s, bool nt) {
     if (p.nb >= 2 && p.xq && p.xqs) {
       // quantise once per launch, then the GEMV copies the codes (no per-block prologue)
       const int lpg = p.gs / 16;
-      if (p.K <= 3 * 256 * 16) {
+      if (p.xq_ready) {
+        // the producer (attention, forward.hip) already stored codes + scales; nb <= 8 there
+      } else if (p.K <= 3 * 256 * 16) {
         if (lpg == 2) hipLaunchKernelGGL(gemv_q8_prequant_reg_kernel<2>, dim3(p.nb), dim3(256), 0, s, p);
         else if (lpg == 4) hipLaunchKernelGGL(gemv_q8_prequant_reg_kernel<4>, dim3(p.nb), dim3(256), 0, s, p);
         else hipLaunchKernelGGL(gemv_q8_prequant_reg_kernel<8>, dim3(p.nb), dim3(256), 0, s, p);
