@@ -223,7 +223,11 @@ def main():
                          f"--cpu-baseline-tokens) from BOS (pos 0..{n - 1}) of the same synthetic {mname} "
                          f"{args.dtype} model with oracle/oracle.c (bit-exact "
                          f"{'runq.c' if q8 else 'src/seq.cpp'} restatement), {cores} thread(s)",
-               "tokens_match_gpu": ctoks == gtoks}
+               "tokens_match_gpu": ctoks == gtoks,
+               # int8 is tolerance parity (runq's per-group float sums in another order), so a
+               # random-init model's greedy path may flip at a near-tie: report how far it agrees
+               "tokens_match_prefix": next((i for i, (a, b) in enumerate(zip(ctoks, gtoks)) if a != b),
+                                           min(len(ctoks), len(gtoks)))}
         ref.close()
 
     if rank == 0:

@@ -126,6 +126,9 @@ struct thallama_decoder {
   float* xn_d = nullptr;        // [<=16][dim] normed rows for the matrix-core GEMV (batch >= 2)
   signed char* xq_d = nullptr;  // int8 batched: activations quantised once per launch [8][max(dim, hidden)]
   float* xqs_d = nullptr;       //   and their group scales
+  signed char* hq_d = nullptr;  // int8 4..8 sequences: SwiGLU output quantised for W2 [8][hidden]
+  float* hqs_d = nullptr;       //   its group scales
+  unsigned* hcnt_d = nullptr;   //   and one ticket per 64-row group (zero between launches)
   float* mpart_d = nullptr;     // matrix-core GEMV split-K partial tiles
   unsigned* mcnt_d = nullptr;   //   and their tickets
   float* part_d = nullptr;      // attention partials [B][H][<=16 units][hs+4]
@@ -318,6 +321,9 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   (void)hipFree(d->mpart_d);
   (void)hipFree(d->xq_d);
   (void)hipFree(d->xqs_d);
+  (void)hipFree(d->hq_d);
+  (void)hipFree(d->hqs_d);
+  (void)hipFree(d->hcnt_d);
   (void)hipFree(d->mcnt_d);
   (void)hipFree(d->part_d);
   (void)hipFree(d->cnt_d);
@@ -371,8 +377,10 @@ static hipError_t gemv(thallama_decoder* d, int mode, tl::GemvParams& p, const Q
   p.Q2 = t2 ? t2->q : nullptr;
   p.S2 = t2 ? t2->s : nullptr;
   p.gs = d->w8.group_size;
-  p.xq = d->xq_d;
-  p.xqs = d->xqs_d;
+  if (!p.xq) {
+    p.xq = d->xq_d;
+    p.xqs = d->xqs_d;
+  }
   return tl::launch_gemv_q8(mode, p, d->stream, d->nt);
 }
 #define Q8L(name) (d->q8 ? &d->w8.name[l] : nullptr)
@@ -383,6 +391,18 @@ static hipError_t gemv(thallama_decoder* d, int mode, tl::GemvParams& p, const Q
 static int q8_attn_quant(const thallama_decoder* d) {
   return d->q8 && d->xq_d && d->B >= 2 && d->B <= 8 && d->w8.group_size == 64 &&
          (d->hs == 64 || d->hs == 128 || d->hs == 256) && (d->dim % 64) == 0;
+}
+
+// int8 decoder, 4..8 sequences on the matrix-core kernel: the W1/W3 + SwiGLU launch stores its
+// output quantised as well (gemv_q8_mfma.hpp), so W2 skips its quantise pass.  Opt-in
+// (THALLAMA_Q8_FFN_QUANT=1): the group hand-off (write-through, ticket, read-back) adds ~5 us
+// to the SwiGLU launch's tail, about what the skipped 4.8 us pass saved.
+static int q8_ffn_quant(const thallama_decoder* d) {
+  static const bool on = [] {
+    const char* e = getenv("THALLAMA_Q8_FFN_QUANT");
+    return e && atoi(e) != 0;
+  }();
+  return on && d->q8 && tl::q8_swiglu_quant_ok(d->B, d->w8.group_size, d->dim, d->hidden);
 }
 
 // Enqueue one decode step reading tok_d / pos_d; logits land in s.logits.
@@ -520,6 +540,11 @@ static int enqueue_step(thallama_decoder* d) {
       p.xn = d->xn_d;
       p.y = s.hb;
       p.y_stride = hid;
+      if (d->hq_d) {
+        p.yq = d->hq_d;
+        p.yqs = d->hqs_d;
+        p.gcnt = d->hcnt_d;
+      }
       int ev = prof_begin(d);
       TL_TRY(gemv(d, tl::GM_SWIGLU, p, Q8L(w1), Q8L(w3), nullptr));
       prof_end(d, THALLAMA_K_FFN_UP, ev);
@@ -535,6 +560,11 @@ static int enqueue_step(thallama_decoder* d) {
       p.x_stride = hid;
       p.y = s.x;
       p.y_stride = dim;
+      if (d->hq_d) {
+        p.xq = d->hq_d;
+        p.xqs = d->hqs_d;
+        p.xq_ready = 1;
+      }
       int ev = prof_begin(d);
       TL_TRY(gemv(d, tl::GM_RESID, p, Q8L(w2), nullptr, nullptr));
       prof_end(d, THALLAMA_K_FFN_DOWN, ev);
@@ -888,6 +918,12 @@ extern "C" int thallama_decoder_create_q8(thallama_decoder** out, const Config* 
     const size_t kmax = (size_t)(d->dim > d->hidden ? d->dim : d->hidden);
     TL_TRY(hipMalloc(&d->xq_d, 8 * kmax));
     TL_TRY(hipMalloc(&d->xqs_d, sizeof(float) * 8 * (kmax / 16 + 1)));
+    if (q8_ffn_quant(d)) {
+      TL_TRY(hipMalloc(&d->hq_d, 8 * (size_t)d->hidden));
+      TL_TRY(hipMalloc(&d->hqs_d, sizeof(float) * 8 * (size_t)(d->hidden / 64)));
+      TL_TRY(hipMalloc(&d->hcnt_d, sizeof(unsigned) * (size_t)(d->hidden / 64)));
+      TL_TRY(hipMemset(d->hcnt_d, 0, sizeof(unsigned) * (size_t)(d->hidden / 64)));
+    }
   }
   // persistent step with int8 weights: re-check the shape (group size, LDS) and publish the
   // per-layer tensor addresses as a device table the kernel indexes by (tensor, layer)

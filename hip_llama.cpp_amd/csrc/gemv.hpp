@@ -73,6 +73,11 @@ struct GemvParams {
   signed char* xq;
   float* xqs;
   int xq_ready;  // xq/xqs already hold this launch's quantised activations (attention wrote them)
+  // int8 matrix-core SwiGLU launch only: also store the output quantised for W2 ([nb][n_items]
+  // codes, [nb][n_items/64] scales; n_items % 64 == 0), with one zeroed ticket per 64-row group
+  signed char* yq;
+  float* yqs;
+  unsigned* gcnt;
   // optional split-K scratch for the matrix-core path: per-block partial tiles
   // [tiles][splits][2][256] and one ticket per tile (zero between launches)
   float* mpart;
