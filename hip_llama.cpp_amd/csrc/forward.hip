@@ -141,6 +141,7 @@ struct thallama_decoder {
   bool profile = false;
   bool persist = true;          // requested (THALLAMA_OPT_PERSISTENT)
   bool pfault = false;          // test hook: the next persistent launch loses block 0
+  bool pasync = false;          // an asynchronous greedy call ran persistent launches not yet checked
   hipGraphExec_t exec = nullptr;
   // persistent one-launch step (persist.hip)
   int ncu = 0;
@@ -664,6 +665,7 @@ static int check_persist(thallama_decoder* d) {
 }
 
 extern "C" int thallama_decoder_persistent(thallama_decoder* d) { return d && use_persist(d) ? 1 : 0; }
+extern "C" int thallama_persistent_cooperative(void) { return tl::persistent_cooperative() ? 1 : 0; }
 
 // Timeline of the persistent step (tools/persist_trace.py): enable allocates the buffer;
 // every later launch overwrites it; copy returns [grid][5L+1][kTraceSlots] 100-MHz stamps.
@@ -693,7 +695,23 @@ static int enqueue_argmax(thallama_decoder* d) {
   return 0;
 }
 
+// An asynchronous greedy call (sync = 0, no tokens requested) returns before its launches run,
+// so a persistent give-up inside it is found only at the next synchronisation: that call's
+// tokens and K/V rows are then invalid, and the error is reported for IT (kPersistAsyncLost),
+// never silently repaired by re-running a later call.
+constexpr int kPersistAsyncLost = (int)hipErrorIllegalState;
+
+static int check_async(thallama_decoder* d) {
+  if (!d->pasync) return 0;
+  d->pasync = false;
+  if (check_persist(d) == 0) return 0;
+  g_last_error = "persistent step: an earlier asynchronous greedy call gave up (grid not co-resident); its tokens "
+                 "and K/V rows are invalid; path disabled";
+  return kPersistAsyncLost;
+}
+
 static int upload_tok_pos(thallama_decoder* d, const int* token_h, const int* pos_h) {
+  int r = 0;
   for (int b = 0; b < d->B; ++b) {
     if (pos_h[b] < 0 || pos_h[b] >= d->S || token_h[b] < 0 || token_h[b] >= d->V) {
       g_last_error = "token/pos out of range";
@@ -702,6 +720,8 @@ static int upload_tok_pos(thallama_decoder* d, const int* token_h, const int* po
   }
   // the staging buffers may still feed an in-flight copy of the previous call
   TL_TRY(hipStreamSynchronize(d->stream));
+  r = check_async(d);
+  if (r) return r;
   memcpy(d->tok_h, token_h, sizeof(int) * d->B);
   memcpy(d->pos_h, pos_h, sizeof(int) * d->B);
   TL_TRY(hipMemcpyAsync(d->tok_d, d->tok_h, sizeof(int) * d->B, hipMemcpyHostToDevice, d->stream));
@@ -794,6 +814,7 @@ static int decoder_greedy_once(thallama_decoder* d, const int* token0_h, const i
   } else if (sync) {
     TL_TRY(hipStreamSynchronize(d->stream));
   } else {
+    d->pasync = d->pasync || (n_steps > 0 && use_persist(d));
     prof_collect(d);
     return 0;
   }
@@ -806,7 +827,15 @@ extern "C" int thallama_decoder_logits(thallama_decoder* d, float* logits_h) {
   TL_TRY(hipMemcpyAsync(logits_h, d->s.logits, sizeof(float) * (size_t)d->B * d->V, hipMemcpyDeviceToHost,
                         d->stream));
   TL_TRY(hipStreamSynchronize(d->stream));
-  return 0;
+  return check_async(d);
+}
+
+// Synchronise the decoder's stream and report a give-up of an earlier asynchronous call.
+extern "C" int thallama_decoder_sync(thallama_decoder* d) {
+  if (!d) return (int)hipErrorInvalidValue;
+  TL_TRY(hipStreamSynchronize(d->stream));
+  prof_collect(d);
+  return check_async(d);
 }
 
 extern "C" int thallama_decoder_prof(thallama_decoder* d, int kclass, double* total_ms, long long* count) {

@@ -31,6 +31,8 @@
 // (e.g. x is rewritten by W2(l) only after every block published hb(l), i.e. finished
 // staging x for W1/W3(l)); see DESIGN.md.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
+#include <mutex>
 #include "attention.hpp"
 #include "gemv.hpp"
 #include "gemv_q8.hpp"
@@ -858,12 +860,21 @@ bool persistent_prepare(PStep& p, int ncu, const char** why) {
   if ((long long)p.dim * (100 + kXcdSkew) / part_weight(ncu) + 2 > kPResidFloats)
     return fail("residual slice per block too large");
   if (lds_bytes(p) > 160 * 1024) return fail("activations do not fit the LDS");
-  static bool attr_set = false;
-  if (!attr_set) {  // allow more than 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
-    for (const void* f : {kfn<128, false>(), kfn<64, false>(), kfn<128, true>(), kfn<64, true>()})
-      if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-        return fail("cannot raise the dynamic LDS limit");
-    attr_set = true;
+  {  // allow more than 64 KiB of dynamic LDS (gfx950: 160 KiB per CU): a per-device attribute,
+     // raised once for each device a decoder is prepared on (decoders of several devices may be
+     // created from several threads, app/run.cpp)
+    static std::mutex mu;
+    static unsigned long long done = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return fail("no current device");
+    std::lock_guard<std::mutex> lock(mu);
+    const unsigned long long bit = dev < 64 ? 1ull << dev : 0ull;
+    if (!bit || !(done & bit)) {
+      for (const void* f : {kfn<128, false>(), kfn<64, false>(), kfn<128, true>(), kfn<64, true>()})
+        if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+          return fail("cannot raise the dynamic LDS limit");
+      done |= bit;
+    }
   }
   int nb = 0;
   const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel_of(p), PT, lds_bytes(p));
@@ -871,8 +882,32 @@ bool persistent_prepare(PStep& p, int ncu, const char** why) {
   return true;
 }
 
+// Co-residency of the grid (one block per CU, spin-waiting on each other's hand-offs) is
+// GUARANTEED by a cooperative launch: the runtime dispatches it on a cooperative queue, which
+// starts the grid only when every block can be resident at once, and refuses (hipErrorCooperative
+// LaunchTooLarge) a grid that could never be.  The bounded waits stay as a second line of
+// defence.  THALLAMA_PERSIST_COOP=0 selects a plain launch (measurement only).
+static bool use_cooperative() {
+  static const bool on = [] {
+    const char* e = getenv("THALLAMA_PERSIST_COOP");
+    int dev = 0, coop = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess)
+      coop = 0;
+    return coop != 0 && !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+bool persistent_cooperative() { return use_cooperative(); }
+
 // The caller zeroes p.sync (kPSyncWords) and the tickets on the same stream right before.
 hipError_t launch_persistent_step(const PStep& p, hipStream_t s, int ncu) {
+  if (use_cooperative()) {
+    PStep arg = p;
+    void* args[] = {&arg};
+    return hipLaunchCooperativeKernel(kernel_of(p), dim3(ncu), dim3(PT), args, (unsigned)lds_bytes(p), s);
+  }
   if (p.q8) {
     if (p.hs == 128) hipLaunchKernelGGL((persistent_step_kernel<128, true>), dim3(ncu), dim3(PT), lds_bytes(p), s, p);
     else hipLaunchKernelGGL((persistent_step_kernel<64, true>), dim3(ncu), dim3(PT), lds_bytes(p), s, p);

@@ -50,5 +50,7 @@ bool persistent_prepare(PStep& p, int ncu, const char** why);
 // Launch only: the caller zeroes p.sync (kPSyncWords) on stream s right before (a memset
 // node ahead of the kernel node when captured).
 hipError_t launch_persistent_step(const PStep& p, hipStream_t s, int ncu);
+// True if launch_persistent_step uses a cooperative launch (co-residency guaranteed).
+bool persistent_cooperative();
 
 }  // namespace tl

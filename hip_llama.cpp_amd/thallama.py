@@ -154,12 +154,14 @@ def lib():
             "thallama_decoder_destroy": (None, [VP]),
             "thallama_decoder_set": (I, [VP, I, I]),
             "thallama_decoder_persistent": (I, [VP]),
+            "thallama_persistent_cooperative": (I, []),
             "thallama_decoder_prefill": (I, [VP, I, c_int_p, I, I]),
             "thallama_decoder_ptrace": (I, [VP, I, C.POINTER(C.c_ulonglong), C.c_size_t]),
             "thallama_decoder_stream": (VP, [VP]),
             "thallama_decoder_forward": (I, [VP, c_int_p, c_int_p, P]),
             "thallama_decoder_greedy": (I, [VP, c_int_p, c_int_p, I, c_int_p, I]),
             "thallama_decoder_logits": (I, [VP, P]),
+            "thallama_decoder_sync": (I, [VP]),
             "thallama_decoder_prof": (I, [VP, I, C.POINTER(C.c_double), C.POINTER(C.c_longlong)]),
             "thallama_decoder_prof_reset": (None, [VP]),
             "thallama_step_bytes": (C.c_double, [C.POINTER(Config), I, I, c_int_p]),
@@ -423,6 +425,10 @@ class Decoder:
         if want_tokens:
             return np.frombuffer(out, dtype=np.int32).reshape(n_steps, self.batch).copy()
         return None
+
+    def sync(self):
+        """Wait for queued work; raises if an earlier asynchronous call's persistent step gave up."""
+        check(lib().thallama_decoder_sync(self.h), "decoder_sync")
 
     def logits(self):
         out = np.empty(self.batch * self.vocab, dtype=np.float32)

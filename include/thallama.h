@@ -44,6 +44,9 @@ enum {
 /* 1 if the decoder runs its steps as one persistent launch (THALLAMA_OPT_PERSISTENT
  * requested and the shape supported), else 0. */
 int thallama_decoder_persistent(thallama_decoder* d);
+/* 1 if the persistent step is dispatched as a cooperative launch (grid co-residency guaranteed
+ * by the runtime), 0 for a plain launch (THALLAMA_PERSIST_COOP=0 or no device support). */
+int thallama_persistent_cooperative(void);
 /* Diagnostics: enable != 0 allocates a timeline buffer that every later persistent launch
  * fills with 100-MHz clock stamps, [grid][5*n_layers+1][4] (phase start, input staged,
  * slots reduced, epilogue drained); host != NULL copies up to n stamps out (synchronous).
@@ -77,8 +80,10 @@ int thallama_decoder_forward(thallama_decoder* d, const int* token_h, const int*
 
 /* Greedy decode n_steps on the device.  Sequence b starts from token0_h[b] at
  * pos0_h[b]; step i writes the argmax token of every sequence to
- * tokens_out_h[i*batch + b] (may be NULL).  Asynchronous unless sync != 0.
- * Returns 0 on success. */
+ * tokens_out_h[i*batch + b] (may be NULL).  Asynchronous unless sync != 0 (or tokens are
+ * requested).  Returns 0 on success.  A persistent step that gave up inside an asynchronous
+ * call is reported by the next call on the decoder (hipErrorIllegalState: that call's tokens
+ * and K/V rows are invalid). */
 int thallama_decoder_greedy(thallama_decoder* d, const int* token0_h, const int* pos0_h, int n_steps,
                             int* tokens_out_h, int sync);
 
@@ -92,6 +97,9 @@ int thallama_decoder_prefill(thallama_decoder* d, int b, const int* tokens_h, in
 
 /* Copy the device logits of the last step into logits_h[batch*vocab] (synchronous). */
 int thallama_decoder_logits(thallama_decoder* d, float* logits_h);
+
+/* Wait for the decoder's queued work; reports an earlier asynchronous call's give-up. */
+int thallama_decoder_sync(thallama_decoder* d);
 
 /* Profiling (THALLAMA_OPT_PROFILE=1): accumulated ms and launch count per kernel class
  * since the last reset. */

@@ -16,6 +16,7 @@
  * The matmul row loop may run on several OpenMP threads: each row's sum is
  * still sequential, so results do not depend on the thread count.
  */
+#define _GNU_SOURCE
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -51,6 +52,7 @@ typedef struct {
   OQT *q_tok, *q_wq, *q_wk, *q_wv, *q_wo, *q_w1, *q_w2, *q_w3, *q_wcls;
   OQT xq, hq;
   float *k, *v;
+  int view; /* 1: a second decoder over another model's weights (owns its RunState only) */
 } OModel;
 
 static int g_threads = 1;
@@ -250,6 +252,13 @@ int oracle_write_v0(OModel* m, const char* path) {
 
 void oracle_model_free(OModel* m) {
   if (!m) return;
+  if (m->view) {
+    free(m->x); free(m->xb); free(m->xb2); free(m->hb); free(m->hb2); free(m->q);
+    free(m->att); free(m->logits); free(m->kc); free(m->vc); free(m->k); free(m->v);
+    free(m->xq.q); free(m->xq.s); free(m->hq.q); free(m->hq.s);
+    free(m);
+    return;
+  }
   free(m->arena);
   free(m->x); free(m->xb); free(m->xb2); free(m->hb); free(m->hb2); free(m->q);
   free(m->att); free(m->logits); free(m->kc); free(m->vc); free(m->k); free(m->v);
@@ -512,6 +521,82 @@ int oracle_q8_greedy(OModel* m, int token, int pos0, int n, int* out) {
     out[i] = token;
   }
   return 0;
+}
+
+/* ------------------------------------------------------------ CPU baseline, aggregate mode */
+/* BASELINE.md CPU-baseline plan (ii): P independent single-threaded decoders, one per core, over
+ * disjoint sequences (decoder i starts from token 1 + i at pos 0), sharing one copy of the
+ * weights; each is the unchanged single-sequence forward above with its own RunState. */
+OModel* oracle_model_view(OModel* m) {
+  OModel* v = calloc(1, sizeof(OModel));
+  if (!v) return NULL;
+  *v = *m; /* weight pointers */
+  v->view = 1;
+  v->x = v->xb = v->xb2 = v->hb = v->hb2 = v->q = v->att = v->logits = v->kc = v->vc = v->k = v->v = NULL;
+  v->xq.q = v->hq.q = NULL;
+  v->xq.s = v->hq.s = NULL;
+  if (!alloc_state(v)) { oracle_model_free(v); return NULL; }
+  if (m->q8arena) {
+    v->xq.q = calloc(m->c.dim, 1); v->xq.s = calloc(m->c.dim, 4);
+    v->hq.q = calloc(m->c.hidden_dim, 1); v->hq.s = calloc(m->c.hidden_dim, 4);
+  }
+  return v;
+}
+
+#include <pthread.h>
+#include <sched.h>
+#include <time.h>
+
+typedef struct {
+  OModel* m;
+  int q8, cpu, start, n;
+  int* out;
+} OAggJob;
+
+static void* agg_worker(void* a) {
+  OAggJob* j = (OAggJob*)a;
+  if (j->cpu >= 0) {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(j->cpu, &set);
+    pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+  }
+  if (j->q8) oracle_q8_greedy(j->m, j->start, 0, j->n, j->out);
+  else oracle_greedy(j->m, j->start, 0, j->n, j->out);
+  return NULL;
+}
+
+/* Runs P decoders of n greedy tokens each at once (decoder i pinned to cpus[i % ncpu], or
+ * unpinned when ncpu == 0); out[P][n] receives the tokens.  Returns the wall time in seconds,
+ * or -1 on an allocation failure. */
+double oracle_aggregate(OModel* m, int q8, int P, const int* cpus, int ncpu, int n, int* out) {
+  OAggJob* jobs = calloc(P, sizeof(OAggJob));
+  pthread_t* th = calloc(P, sizeof(pthread_t));
+  const int saved = g_threads;
+  double secs = -1.0;
+  int ok = jobs && th;
+  for (int i = 0; ok && i < P; ++i) {
+    jobs[i].m = oracle_model_view(m);
+    ok = jobs[i].m != NULL;
+    jobs[i].q8 = q8; jobs[i].cpu = ncpu > 0 ? cpus[i % ncpu] : -1;
+    jobs[i].start = 1 + i % (m->c.vocab_size - 1); jobs[i].n = n; jobs[i].out = out + (size_t)i * n;
+  }
+  if (ok) {
+    g_threads = 1; /* each decoder single-threaded, like seq.cpp */
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    int started = 0;
+    for (; started < P; ++started)
+      if (pthread_create(&th[started], NULL, agg_worker, &jobs[started]) != 0) break;
+    for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    g_threads = saved;
+    if (started == P) secs = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+  }
+  for (int i = 0; jobs && i < P; ++i) oracle_model_free(jobs[i].m);
+  free(jobs);
+  free(th);
+  return secs;
 }
 
 /* The synthetic generator, exposed so tests can check the device filler bit-for-bit. */

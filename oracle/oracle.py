@@ -77,6 +77,7 @@ def lib():
             "oracle_q8_forward": (F, [V, C.c_int, C.c_int]),
             "oracle_q8_greedy": (C.c_int, [V, C.c_int, C.c_int, C.c_int, IP]),
             "oracle_synth_fill": (None, [F, S, U64, C.c_int, C.c_double, S]),
+            "oracle_aggregate": (C.c_double, [V, C.c_int, C.c_int, IP, C.c_int, C.c_int, IP]),
         }
         for n, (r, a) in sig.items():
             fn = getattr(L, n)
@@ -233,6 +234,18 @@ class Model:
         out = (C.c_int * n)()
         lib().oracle_q8_greedy(self.h, token, pos0, n, out)
         return list(out)
+
+    def aggregate(self, P, n, cpus=None):
+        """BASELINE.md CPU-baseline mode (ii): P independent single-threaded decoders (decoder i
+        from token 1+i at pos 0, pinned to cpus[i % len(cpus)]) of n greedy tokens each, at once,
+        over these weights.  Returns (wall seconds, tokens [P][n])."""
+        cpus = list(cpus or [])
+        cp = (C.c_int * max(1, len(cpus)))(*cpus) if cpus else None
+        out = (C.c_int * (P * n))()
+        secs = lib().oracle_aggregate(self.h, int(self.q8), P, cp, len(cpus), n, out)
+        if secs < 0:
+            raise MemoryError("oracle_aggregate")
+        return secs, np.array(list(out), np.int32).reshape(P, n)
 
     def close(self):
         if self.h:

@@ -80,6 +80,31 @@ def test_give_up_falls_back(gpu, oracle, graph):
     assert not dec.persistent()
 
 
+def test_async_give_up_is_reported(gpu, oracle):
+    """An asynchronous greedy call (sync=0, no tokens) returns before its launches run: a give-up
+    inside it must be reported by the next call on the decoder (its tokens and K/V rows are
+    invalid), not silently repaired by re-running only the later call."""
+    _, _, _, dec = decoder(gpu, SMALL, 0, 42, 1)
+    dec.set(gpu.OPT_USE_GRAPH, 1)
+    want = oracle.Model(SMALL, 0, seed=42).greedy(1, 0, 12)
+    assert dec.greedy([1], [0], 4)[:, 0].tolist() == want[:4]
+    dec.set(gpu.OPT_PERSIST_FAULT, 1)
+    dec.greedy([want[3]], [4], 4, want_tokens=False, sync=False)
+    with pytest.raises(RuntimeError):
+        dec.sync()
+    assert not dec.persistent()
+    # the caller re-runs the lost call itself; the multi-launch path then gives the oracle's tokens
+    assert dec.greedy([want[3]], [4], 8)[:, 0].tolist() == want[4:12]
+
+
+def test_cooperative_launch(gpu):
+    """The persistent grid is dispatched as a cooperative launch (co-residency guaranteed by the
+    runtime) on MI355X unless THALLAMA_PERSIST_COOP=0."""
+    import os
+    if os.environ.get("THALLAMA_PERSIST_COOP", "1") != "0":
+        assert gpu.lib().thallama_persistent_cooperative() == 1
+
+
 @pytest.mark.parametrize("cfg", [SMALL, HEAD128, RAGGED])
 def test_forced_logits_every_step(gpu, oracle, cfg):
     _, _, _, dec = decoder(gpu, cfg, 0, 9, 1)
