@@ -173,7 +173,7 @@ static std::vector<Replica> replicate(ModelFile& m, int n_dev, int batch) {
     HIP_OK(hipSetDevice(d));
     Replica& r = reps[d];
     r.dev = d;
-    alloc_state_to_device_batch(&m.t, &r.s, batch);
+    alloc_state_to_device_batch(&m.t, r.s, batch);
     int rc;
     if (m.q8) {
       HIP_OK(hipMalloc(&r.emb, sizeof(float) * (size_t)m.cfg.vocab_size * m.cfg.dim));

@@ -918,12 +918,41 @@ extern "C" thablasStatus_t thaDNN_s_forward_batch(thablasHandle_t handle1, thabl
       dec_cache()[key] = d;
     }
   }
-  int r = thallama_decoder_forward(d, token, pos, logits_host);
+  // The reference's scheduler (src/llama.cpp:961-1017) runs every slot of the batch, and a slot
+  // that never received a request carries uninitialised token/pos; its kernel would read out of
+  // bounds.  Such slots run as token 0 at position 0 here: they write only their own K/V row 0,
+  // which a request later admitted to the slot rewrites at its first step, and their logits are
+  // never read.
+  std::vector<int> tk(token, token + n_batches), ps(pos, pos + n_batches);
+  for (int b = 0; b < n_batches; ++b)
+    if (tk[b] < 0 || tk[b] >= d->V || ps[b] < 0 || ps[b] >= d->S) tk[b] = ps[b] = 0;
+  int r = thallama_decoder_forward(d, tk.data(), ps.data(), logits_host);
   if (r) {
     fprintf(stderr, "thaDNN_s_forward_batch: %s\n", thallama_last_error());
     return r == (int)hipErrorInvalidValue ? THABLAS_STATUS_INVALID_VALUE : THABLAS_STATUS_EXECUTION_FAILED;
   }
   return THABLAS_STATUS_SUCCESS;
+}
+
+// Out of scope: the reference's 70B and pipeline drivers (src/thaDNN.cpp:83-427).
+extern "C" thablasStatus_t thaDNN_s_forward_70B(thablasHandle_t, int, Config*, TransformerWeights*[], RunState*,
+                                               TransformerWeights*, RunState*, int[], int[], float*) {
+  return THABLAS_STATUS_NOT_SUPPORTED;
+}
+extern "C" thablasStatus_t thaDNN_s_forward_batch_pipe_line(thablasHandle_t[], int, int, Transformer*[], int[], int[],
+                                                           float*) {
+  return THABLAS_STATUS_NOT_SUPPORTED;
+}
+extern "C" thablasStatus_t thaDNN_s_forward_batch_multiple_pipe_line(thablasHandle_t[], int, int, int, int, Config*,
+                                                                    TransformerWeights*[], RunState*[], int[], int[],
+                                                                    float*, int*, int*, THALLAMA_OMP_LOCK*) {
+  return THABLAS_STATUS_NOT_SUPPORTED;
+}
+extern "C" thablasStatus_t thaDNN_s_forward_batch_multiple_pipe_line_layer_swap(thablasHandle_t[], int, int, int, int,
+                                                                               int, Config*, TransformerWeights*[],
+                                                                               RunState*[], RunState*[], int[], int[],
+                                                                               float*, THALLAMA_OMP_LOCK*) {
+  return THABLAS_STATUS_NOT_SUPPORTED;
 }
 
 // ------------------------------------------------------------------ int8 (runq Q8_0) decoder

@@ -83,13 +83,43 @@ void free_run_state(RunState* s);
 void free_transformer(Transformer* t);
 void print_transformer(Transformer* t);
 
-// ---- device residency (reference src/models.cpp:86-179).  Unlike the reference, the
-// weights live in ONE device arena laid out exactly like the file payload, so a single
-// H2D copy (or one RCCL broadcast) moves the whole model.
-void copy_weight_to_device(Transformer* t_h, TransformerWeights** w_d);
-void alloc_state_to_device_batch(Transformer* t_h, RunState** s_d_batch, int batch_size);
+// ---- device residency (reference include/models.hpp:120-134, src/models.cpp:86-179).  Unlike
+// the reference, the weights live in ONE device arena laid out exactly like the file payload,
+// so a single H2D copy (or one RCCL broadcast) moves the whole model.  The out-parameters are
+// the reference's C++ references (`TransformerWeights* &w_d`) for C++ callers, so its
+// src/llama.cpp compiles unchanged; the C ABI (C callers, FFIs) sees the same symbol taking a
+// pointer to the pointer.
+#ifdef __cplusplus
+#define THALLAMA_OUT(T) T*&
+#else
+#define THALLAMA_OUT(T) T**
+#endif
+// reference include/models.hpp:121
+void copy_transformer_to_device(thablasHandle_t handle, Transformer* t_h, THALLAMA_OUT(Transformer) t_d);
+// reference include/models.hpp:122
+void copy_weight_to_device(Transformer* t_h, THALLAMA_OUT(TransformerWeights) w_d);
+// reference include/models.hpp:123 (one sequence)
+void alloc_state_to_device(Transformer* t_h, THALLAMA_OUT(RunState) s_d);
+// reference include/models.hpp:124
+void alloc_state_to_device_batch(Transformer* t_h, THALLAMA_OUT(RunState) s_d_batch, int batch_size);
 void free_weight_device(TransformerWeights* w_d);
 void free_state_device(RunState* s_d);
+
+// ---- out of scope (7B fits one MI355X's 288 GB): the reference's pipeline,
+// layer-swap and 70B host/device staging (include/models.hpp:120, 125-134).  Declared with the
+// reference signatures so its src/llama.cpp links unchanged; they are never reached from its
+// main().  Each prints that it is unsupported and leaves every out-parameter NULL.
+void set_transformer(void);
+void copy_transformer_pipeline_to_device(thablasHandle_t handle, Transformer* t_h, THALLAMA_OUT(Transformer) t_d, int pipe_size, int pipe_id);
+void copy_transformer_pipeline_to_device_batch(thablasHandle_t handle, Transformer* t_h, THALLAMA_OUT(Transformer) t_d, int pipe_size, int pipe_id, int batch_size);
+void copy_transformer_weight_pipeline_to_device_batch(Transformer* t_h, THALLAMA_OUT(TransformerWeights) w_d, int pipe_size, int pipe_id, int batch_size);
+void alloc_run_state_to_device_batch(thablasHandle_t handle, Transformer* t_h, THALLAMA_OUT(RunState) s_d, int pipe_size, int pipe_id, int batch_size);
+void alloc_swap_run_state_on_host_batch(thablasHandle_t handle, Transformer* t_h, THALLAMA_OUT(RunState) s_h, int pipe_size, int pipe_id, int batch_size, int n_buffer_words);
+void alloc_swap_run_state_to_device_batch(thablasHandle_t handle, Transformer* t_h, THALLAMA_OUT(RunState) s_d, int pipe_size, int pipe_id, int batch_size, int n_buffer_words);
+void copy_transformer_to_host_70B(Transformer* storage_t, TransformerWeights* h_w[], RunState* h_s[], int n_devices);
+void alloc_state_to_device_70B(Transformer* t_h, THALLAMA_OUT(RunState) d_s);
+void alloc_weight_to_device_70B(Transformer* h_t, THALLAMA_OUT(TransformerWeights) d_w);
+void free_transformer_device(void);
 
 // Number of floats in the v0 payload after the 28-byte header (including the unused
 // freq_cis block and, when unshared, wcls) — the size of the device arena.
@@ -98,5 +128,20 @@ size_t thallama_v0_payload_floats(const Config* p, int shared_weights);
 void thallama_map_weights(TransformerWeights* w, const Config* p, float* arena, int shared_weights);
 
 #ifdef __cplusplus
-}
+}  // extern "C"
+
+// reference include/models.hpp:72-117: the fp16 mirrors and the paged-KV block (declared by the
+// reference, used by none of its live paths; kept so code naming them still compiles)
+#include <hip/hip_fp16.h>
+typedef struct {
+  float* addr;
+  int occupied;
+} KVBlock;
+typedef struct {
+  __half *token_embedding_table, *rms_att_weight, *rms_ffn_weight, *wq, *wk, *wv, *wo, *w1, *w2, *w3,
+      *rms_final_weight, *wcls;
+} TransformerWeightsHalf;
+typedef struct {
+  __half *x, *xb, *xb2, *hb, *hb2, *q, *k, *v, *att, *logits, *key_cache, *value_cache;
+} RunStateHalf;
 #endif

@@ -8,6 +8,18 @@
 #include "thaDNN/thaDNN_softmax.hpp"
 #include "thaDNN/thaDNN_swiglu.hpp"
 
+#include "utils.hpp"
+// the reference's thaDNN.hpp includes <omp.h> (its pipeline driver takes omp_lock_t*)
+#if defined(__has_include)
+#if __has_include(<omp.h>)
+#include <omp.h>
+#define THALLAMA_OMP_LOCK omp_lock_t
+#endif
+#endif
+#ifndef THALLAMA_OMP_LOCK
+#define THALLAMA_OMP_LOCK void
+#endif
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -37,6 +49,15 @@ thablasStatus_t thaDNN_s_forward_batch(thablasHandle_t handle1, thablasHandle_t 
                                        thablasHandle_t handle3, int n_batches, Config* p,
                                        TransformerWeights* w, RunState* s_batch, int token[],
                                        int pos[], float* logits_host);
+
+// ---- out of scope (7B fits one MI355X): the 70B layer-streaming and the
+// pipeline / layer-swap drivers (reference include/thaDNN.hpp:72-80, src/thaDNN.cpp:83-427),
+// declared with the reference signatures so its src/llama.cpp links unchanged (they are not
+// reached from its main()).  Each returns THABLAS_STATUS_NOT_SUPPORTED.
+thablasStatus_t thaDNN_s_forward_70B(thablasHandle_t handle, int batch_size, Config* p, TransformerWeights* h_w[], RunState* h_s, TransformerWeights* d_w, RunState* d_s, int token[], int pos[], float* logits_host);
+thablasStatus_t thaDNN_s_forward_batch_pipe_line(thablasHandle_t handle[], int n_devices, int n_batches, Transformer* transformer_d[], int token[], int pos[], float* logits_host);
+thablasStatus_t thaDNN_s_forward_batch_multiple_pipe_line(thablasHandle_t handle[], int host_thread_id, int n_host_threads, int n_devices, int batch_size, Config* p, TransformerWeights* w[], RunState* s_batch[], int token[], int pos[], float* logits_host, int* host_thread_status, int* device_host_thread, THALLAMA_OMP_LOCK* device_mtx);
+thablasStatus_t thaDNN_s_forward_batch_multiple_pipe_line_layer_swap(thablasHandle_t handle[], int thread_id, int n_host_threads, int n_devices, int batch_size, int n_buffer_words, Config* p, TransformerWeights* w[], RunState* s_batch[], RunState* s_host_batch[], int token[], int pos[], float* logits_host, THALLAMA_OMP_LOCK* device_locks);
 
 #ifdef __cplusplus
 }

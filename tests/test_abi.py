@@ -20,6 +20,8 @@ def declared_functions(host=False):
     for h in glob.glob(os.path.join(REPO, "include", "**", "*.h*"), recursive=True):
         if h.endswith("thallama_synth.h") or h.endswith("hip_helper.hpp"):
             continue  # header-only helpers / macros
+        if h.endswith(("seq.hpp", "utils.hpp")):
+            continue  # caller-side declarations, defined by the caller's own src/seq.cpp / src/utils.cpp
         if h.endswith(HOST_HEADERS) != host:
             continue
         src = open(h).read()
