@@ -112,3 +112,27 @@ done:
 #undef CK
   return (int)err;
 }
+
+// ---- test hook: the wave-parallel left-to-right sum (seqsum.hpp) on `count` arrays of n floats
+// (device pointers), one wave each; tests/test_seqsum_gpu.py compares with the sequential chain.
+#include "seqsum.hpp"
+__global__ void __launch_bounds__(64) k_seqsum_check(const float* in, int n, float* out) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const float* a = in + (size_t)blockIdx.x * n;
+  const int ch = tl::seqsum_ch(n);
+  for (int i = threadIdx.x; i < tl::seqsum_floats(n); i += 64) lds[i] = 0.f;
+  __syncthreads();
+  for (int e = threadIdx.x; e < n; e += 64) lds[tl::seqsum_index(e, ch)] = a[e];
+  __syncthreads();
+  const float s = tl::wave_seqsum(lds, n, threadIdx.x);
+  if (threadIdx.x == 0) out[blockIdx.x] = s;
+}
+
+extern "C" int thallama_seqsum_check(const float* in_d, int n, int count, float* out_d) {
+  if (!in_d || !out_d || n <= 0 || n > 8192 || count <= 0) return (int)hipErrorInvalidValue;
+  const size_t lds = sizeof(float) * 64 * (4 * ((n + 255) / 256) + 4);
+  hipLaunchKernelGGL(k_seqsum_check, dim3(count), dim3(64), lds, 0, in_d, n, out_d);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  return (int)e;
+}

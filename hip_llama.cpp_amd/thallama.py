@@ -175,6 +175,7 @@ def lib():
             "thallama_memcpy_d2d": (I, [VP, VP, S]),
             "thallama_memset": (I, [VP, I, S]),
             "thallama_sync": (I, []),
+            "thallama_seqsum_check": (I, [VP, I, I, VP]),
             "thallama_last_error": (C.c_char_p, []),
         }
         for name, (res, args) in sig.items():

@@ -117,6 +117,10 @@ double thallama_step_bytes(const Config* cfg, int batch, int kclass, const int* 
 int thallama_gemv_bench(int mode, int M, int K, int nb, int ipw, int waves, int pf, int nt, int iters,
                         double* us_out);
 
+/* Test hook: the wave-parallel left-to-right fp32 sum (csrc/seqsum.hpp) of `count` arrays of n
+ * floats (device in_d, n <= 8192) into out_d[count]; synchronous. */
+int thallama_seqsum_check(const float* in_d, int n, int count, float* out_d);
+
 /* ---- synthetic weights ------------------------------------------------- */
 /* Fill a v0 arena (layout of thallama_map_weights) with the deterministic synthetic
  * model: N(0,0.02)-shaped linears/embedding, wo & w3 scaled by 1/sqrt(2L), norms 1,
