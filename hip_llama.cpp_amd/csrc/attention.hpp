@@ -9,6 +9,8 @@
 // read by hs/4 lanes with one float4 each.
 #pragma once
 #include "common.hpp"
+#include "libm_exact.hpp"
+#include "seqsum.hpp"
 
 namespace tl {
 
@@ -71,7 +73,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p) {
   m = block_max(m, red);
   float l = 0.f;
   for (int i = tid; i < n; i += 256) {
-    float e = expf(__fsub_rn(sc[i], m));
+    float e = expf_libm(__fsub_rn(sc[i], m));
     sc[i] = e;
     l += e;
   }
@@ -387,13 +389,13 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane)
     float pr;
     if (whole) {
       // reference softmax (src/seq.cpp:18-36): exp, sum, divide, then the weighted sum
-      const float e = lane < n ? expf(__fsub_rn(my, mc)) : 0.f;
+      const float e = lane < n ? expf_libm(__fsub_rn(my, mc)) : 0.f;
       pr = __fdiv_rn(e, wave_sum_u(e));
       m = mc;
     } else {
       const float mn = fmaxf(m, mc);
-      const float e = lane < n ? expf(__fsub_rn(my, mn)) : 0.f;
-      const float scale = expf(__fsub_rn(m, mn));  // rescale what earlier chunks summed
+      const float e = lane < n ? expf_libm(__fsub_rn(my, mn)) : 0.f;
+      const float scale = expf_libm(__fsub_rn(m, mn));  // rescale what earlier chunks summed
       l = fmaf(l, scale, wave_sum_u(e));
 #pragma unroll
       for (int c = 0; c < VPL; ++c) o[c] *= scale;
@@ -446,7 +448,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane)
     for (int c = 0; c < VPL; ++c) ov[k][c] = ld_sc1(recs + kk * (HS + 4) + lane * VPL + c);
   }
   const float M = wave_max_u(lane < nact ? mk : -3.402823466e+38f);
-  const float sk = lane < nact ? expf(__fsub_rn(mk, M)) : 0.f;
+  const float sk = lane < nact ? expf_libm(__fsub_rn(mk, M)) : 0.f;
   const float L = wave_sum_u(lk * sk);
   float acc[VPL];
 #pragma unroll
@@ -474,6 +476,136 @@ __global__ void __launch_bounds__(64) attn_wave_kernel(AttnWaveParams w) {
   attn_unit<HS, CH>(w, blockIdx.x, sc, threadIdx.x);
 }
 
+// ---------------------------------------------------------------------------
+// runq's attention, bit for bit (runq.c:396-434; the same order as src/seq.cpp:103-136), for the
+// int8 path: the Wo input is re-quantised, so the head output must be the reference's floats.
+//   score_t = (((0 + q0 k0) + q1 k1) + ...) / sqrtf(hs)      one lane per key, sequential dot
+//   e_t = expf(score_t - max);  sum = e_0 + e_1 + ...         libm_exact.hpp; seqsum.hpp
+//   a_t = e_t / sum;  xb_i = ((0 + a_0 v0_i) + a_1 v1_i) + ...  one lane per output column
+// One full wave per (sequence b, head h).  `strip` (LDS) holds attn_exact_floats(hs, T) floats.
+// GR (persistent step): q and this step's k/v rows come from the granules.  Products and sums
+// are single roundings (no contraction), like the reference compiled without FMA.
+TL_DEVICE int attn_exact_floats(int hs, int T) { return 3 * hs + seqsum_floats(T) + ((T + 3) & ~3) + 64; }
+
+template <int HS, bool GR>
+TL_DEVICE void attn_unit_exact(const AttnWaveParams& w, int b, int h, float* strip, int lane) {
+  constexpr int VPL = HS / 64;
+  const AttnParams& p = w.a;
+  const int T = p.pos[b] + 1;
+  const int kvh = h / p.kv_mul;
+  const float* kbase = p.kc + (long long)b * p.kv_b_stride + p.kv_l_off + (long long)kvh * HS;
+  const float* vbase = p.vc + (long long)b * p.kv_b_stride + p.kv_l_off + (long long)kvh * HS;
+  float* qs = strip;             // q [HS]
+  float* kn = qs + HS;           // k row of position T-1 [HS] (granule mode)
+  float* vn = kn + HS;           // v row of position T-1 [HS]
+  float* sa = vn + HS;           // exp values, seqsum layout
+  float* at = sa + seqsum_floats(T);  // probabilities [T]
+  const int ch = seqsum_ch(T);
+  for (int i = lane; i < seqsum_floats(T); i += 64) sa[i] = 0.f;
+  if constexpr (GR) {
+    // q, k_new, v_new requested together (one round trip), late granules re-polled singly
+    const unsigned long long* src[3] = {w.gqkv + h * HS, w.gqkv + p.dim + kvh * HS,
+                                        w.gqkv + p.dim + p.kv_dim + kvh * HS};
+    float* dst[3] = {qs, kn, vn};
+    unsigned long long g[3][VPL];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < VPL; ++c) g[r][c] = ld8_sc1(src[r] + lane * VPL + c);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < VPL; ++c)
+        dst[r][lane * VPL + c] = (unsigned)(g[r][c] >> 32) == w.tag_in
+                                     ? __uint_as_float((unsigned)g[r][c])
+                                     : gran_wait(src[r] + lane * VPL + c, w.tag_in, w.err);
+    if (w.ts && lane == 0) w.ts[0] = __builtin_amdgcn_s_memrealtime();
+  } else {
+    const float* q = p.q + (long long)b * p.dim + h * HS;
+#pragma unroll
+    for (int c = 0; c < VPL; ++c) qs[lane * VPL + c] = q[lane * VPL + c];
+  }
+  wave_lds_fence();
+  // scores: lane t, t + 64, ... (cached rows; in granule mode row T-1 from the strip)
+  const float rs = sqrtf((float)HS);
+  float mx = -__builtin_inff();
+  for (int t0 = 0; t0 < T; t0 += 64) {
+    const int t = t0 + lane;
+    const int tl = t < T ? t : T - 1;
+    const bool fresh = GR && tl == T - 1;
+    const f4* kr = reinterpret_cast<const f4*>(kbase + (long long)(GR && tl == T - 1 ? (T >= 2 ? T - 2 : 0) : tl) * p.kv_dim);
+    const f4* k2 = reinterpret_cast<const f4*>(kn);
+    const f4* q4 = reinterpret_cast<const f4*>(qs);
+    float sc = 0.f;
+#pragma unroll 4
+    for (int i = 0; i < HS / 4; ++i) {
+      f4 kv = kr[i];
+      if (fresh) kv = k2[i];
+      const f4 qv = q4[i];
+      sc = __fadd_rn(sc, __fmul_rn(qv.x, kv.x));
+      sc = __fadd_rn(sc, __fmul_rn(qv.y, kv.y));
+      sc = __fadd_rn(sc, __fmul_rn(qv.z, kv.z));
+      sc = __fadd_rn(sc, __fmul_rn(qv.w, kv.w));
+    }
+    sc = __fdiv_rn(sc, rs);
+    if (t < T) {
+      at[t] = sc;
+      mx = fmaxf(mx, sc);
+    }
+  }
+  mx = wave_max_u(mx);  // exact (a maximum)
+  wave_lds_fence();
+  for (int t = lane; t < T; t += 64) sa[seqsum_index(t, ch)] = expf_libm(__fsub_rn(at[t], mx));
+  wave_lds_fence();
+  const float sum = wave_seqsum(sa, T, lane);
+  for (int t = lane; t < T; t += 64) at[t] = __fdiv_rn(sa[seqsum_index(t, ch)], sum);
+  wave_lds_fence();
+  // weighted sum of V: lane owns columns lane*VPL + c, a chain over t each
+  float o[VPL];
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) o[c] = 0.f;
+  const int tc = GR ? T - 1 : T;  // rows read from the cache
+  int t = 0;
+  for (; t + 4 <= tc; t += 4) {
+    float vv[4][VPL];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int c = 0; c < VPL; ++c) vv[u][c] = vbase[(long long)(t + u) * p.kv_dim + lane * VPL + c];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float a = at[t + u];
+#pragma unroll
+      for (int c = 0; c < VPL; ++c) o[c] = __fadd_rn(o[c], __fmul_rn(a, vv[u][c]));
+    }
+  }
+  for (; t < tc; ++t) {
+    const float a = at[t];
+#pragma unroll
+    for (int c = 0; c < VPL; ++c) o[c] = __fadd_rn(o[c], __fmul_rn(a, vbase[(long long)t * p.kv_dim + lane * VPL + c]));
+  }
+  if constexpr (GR) {
+    const float a = at[T - 1];
+#pragma unroll
+    for (int c = 0; c < VPL; ++c) o[c] = __fadd_rn(o[c], __fmul_rn(a, vn[lane * VPL + c]));
+    if (w.ts && lane == 0) w.ts[2] = __builtin_amdgcn_s_memrealtime();
+    wave_lds_fence();
+    publish_head<HS>(w, h, o, strip, lane);  // (the strip's q is dead)
+  } else {
+    store_head<HS>(w, b, h, o, lane);
+  }
+  wave_lds_fence();
+}
+
+// Stand-alone launch of the exact unit (int8 multi-launch steps): one 64-thread block per
+// (sequence, head), grid B*H, dynamic LDS attn_exact_floats(HS, max T) floats.
+template <int HS>
+__global__ void __launch_bounds__(64) attn_exact_kernel(AttnWaveParams w) {
+  extern __shared__ __attribute__((aligned(16))) float strip[];
+  const int b = blockIdx.x / w.a.n_heads, h = blockIdx.x % w.a.n_heads;
+  attn_unit_exact<HS, false>(w, b, h, strip, threadIdx.x);
+}
+
 // out[b][h*hs + i] = sum_s o_s[i] e^{m_s-M} / sum_s l_s e^{m_s-M}
 static __global__ void __launch_bounds__(256) attn_combine_kernel(AttnParams p) {
   const int h = blockIdx.x, b = blockIdx.y;
@@ -493,10 +625,10 @@ static __global__ void __launch_bounds__(256) attn_combine_kernel(AttnParams p) 
     ns = s + 1;
   }
   float L = 0.f;
-  for (int s = 0; s < ns; ++s) L += base[s * (hs + 4) + hs + 1] * expf(base[s * (hs + 4) + hs] - M);
+  for (int s = 0; s < ns; ++s) L += base[s * (hs + 4) + hs + 1] * expf_libm(base[s * (hs + 4) + hs] - M);
   for (int i = threadIdx.x; i < hs; i += blockDim.x) {
     float acc = 0.f;
-    for (int s = 0; s < ns; ++s) acc = fmaf(base[s * (hs + 4) + i], expf(base[s * (hs + 4) + hs] - M), acc);
+    for (int s = 0; s < ns; ++s) acc = fmaf(base[s * (hs + 4) + i], expf_libm(base[s * (hs + 4) + hs] - M), acc);
     p.out[(long long)b * p.dim + h * hs + i] = acc / L;
   }
 }

@@ -9,6 +9,11 @@
 
 #define TL_DEVICE __device__ __forceinline__
 
+// IEEE single roundings on this toolchain (clang __clang_hip_math.h): __fadd_rn / __fmul_rn /
+// __fsub_rn are plain + * - (the Makefile's -ffp-contract=off keeps a*b+c two roundings) and
+// __fdiv_rn and sqrtf are correctly rounded, but __fsqrt_rn is the native v_sqrt_f32 (~1 ulp):
+// never use it where the reference's sqrtf must be matched.
+
 namespace tl {
 
 constexpr int kWave = 64;

@@ -667,6 +667,17 @@ static int check_persist(thallama_decoder* d) {
 extern "C" int thallama_decoder_persistent(thallama_decoder* d) { return d && use_persist(d) ? 1 : 0; }
 extern "C" int thallama_persistent_cooperative(void) { return tl::persistent_cooperative() ? 1 : 0; }
 
+// Diagnostics: copy the persistent step's hand-off granules {value, tag} (x | xb | hb | q k v |
+// int8 codes | scales, the last layer's values after a launch) to host (n granules at most).
+extern "C" int thallama_decoder_granules(thallama_decoder* d, unsigned long long* host, size_t n) {
+  if (!d || !d->pgran) return (int)hipErrorInvalidValue;
+  const size_t ng = (size_t)3 * d->dim + d->hidden + 2 * d->kv_dim + d->dim / 4 + d->dim / 64 + 2;
+  if (!host) return (int)ng;
+  TL_TRY(hipStreamSynchronize(d->stream));
+  TL_TRY(hipMemcpy(host, d->pgran, (n < ng ? n : ng) * 8, hipMemcpyDeviceToHost));
+  return (int)ng;
+}
+
 // Timeline of the persistent step (tools/persist_trace.py): enable allocates the buffer;
 // every later launch overwrites it; copy returns [grid][5L+1][kTraceSlots] 100-MHz stamps.
 extern "C" int thallama_decoder_ptrace(thallama_decoder* d, int enable, unsigned long long* host, size_t n) {

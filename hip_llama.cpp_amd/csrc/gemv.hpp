@@ -23,6 +23,7 @@
 #pragma once
 #include <stdlib.h>
 #include "common.hpp"
+#include "libm_exact.hpp"
 
 namespace tl {
 
@@ -98,8 +99,9 @@ inline int mfma_target_blocks() {
 }
 
 TL_DEVICE float silu_mul(float a, float b) {
-  // reference src/seq.cpp:159-166: val *= 1/(1+expf(-val)); val *= hb2
-  float s = __fdiv_rn(1.0f, __fadd_rn(1.0f, expf(-a)));
+  // reference src/seq.cpp:159-166 / runq.c:455-462: val *= 1/(1+expf(-val)); val *= hb2, with
+  // the host libm's expf bit for bit (libm_exact.hpp)
+  float s = __fdiv_rn(1.0f, __fadd_rn(1.0f, expf_libm(-a)));
   return __fmul_rn(__fmul_rn(a, s), b);
 }
 

@@ -63,6 +63,9 @@ TL_LIBM_HD inline uint32_t libm_asu32(float f) {
 TL_LIBM_HD inline double libm_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
 TL_LIBM_HD inline float expf_libm(float x) {
+#if defined(__clang__)
+#pragma clang fp contract(off)  // only the explicit fma below fuse (HIP compiles with contraction on)
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
   constexpr uint64_t T[32] = TL_EXPF_TABLE;
 #else

@@ -290,14 +290,18 @@ TL_DEVICE void load_slot_q8(const PDesc& d, const PGeo& g, const PStep& p, int s
 }
 
 // runq.c:317-342 per chunk: per group the int32 dot (v_dot4_i32_i8 + quad reduce-scatter), then
-// val += ((float)ival * w.s) * x.s; chunk sums land in res in chunk order.
-TL_DEVICE void consume_slot_q8(const PGeo& g, int slot, int lane, const f4 (&buf)[PL], const float (&sc)[PL],
-                               const signed char* xq, const float* xsc, float* res) {
+// the group's ((float)ival * w.s) * x.s (runq.c:336), and the row value as runq's left-to-right
+// chain val = fl(val + product) over the row's groups (runq.c:330-338; a tree over the groups
+// moves last bits, and the int8 path re-quantises every activation — tools/probes/q8drift.c).
+// A row of one chunk (K <= 4096) is chained here: the products go through the wave's LDS
+// scratch `cw` and lanes 0 / 1 chain the slot's two rows into res.  Longer rows (W2) leave their
+// products in pbuf (row stride pgp) and the epilogue chains them.
+TL_DEVICE void consume_slot_q8(const PGeo& g, int K, int slot, int lane, const f4 (&buf)[PL], const float (&sc)[PL],
+                               const signed char* xq, const float* xsc, float* res, float* pbuf, int pgp, float* cw) {
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int Q = 2 * slot + h;
     const int c = Q % g.nch;
-    float a = 0.f;
     int dd[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -317,11 +321,26 @@ TL_DEVICE void consume_slot_q8(const PGeo& g, int slot, int lane, const f4 (&buf
     s1 += __builtin_amdgcn_mov_dpp(b0 ? dd[2] : dd[3], 0xB1, 0xF, 0xF, false);
     int gs = b1 ? s1 : s0;
     gs += __builtin_amdgcn_mov_dpp(b1 ? s0 : s1, 0x4E, 0xF, 0xF, false);       // quad_perm [2,3,0,1]
-    const int grp = c * 64 + (lane & 3) * 16 + (lane >> 2);
-    a = __fmul_rn(__fmul_rn((float)gs, sc[h]), xsc[grp]);  // runq.c:334
-    a = wave_sum_u(a);
-    if (lane == 0 && Q < g.nres) res[Q] = a;
+    const int gi = (lane & 3) * 16 + (lane >> 2);  // group within the chunk
+    const float a = __fmul_rn(__fmul_rn((float)gs, sc[h]), xsc[c * 64 + gi]);  // runq.c:336
+    if (Q < g.nres) {
+      if (g.nch == 1) cw[h * 68 + gi] = a;
+      else pbuf[(Q / g.nch) * pgp + c * 64 + gi] = a;
+    }
     __builtin_amdgcn_sched_barrier(0);
+  }
+  if (g.nch == 1) {
+    wave_lds_fence();
+    if (lane < 2 && 2 * slot + lane < g.nres) {
+      const f4* r = reinterpret_cast<const f4*>(cw + lane * 68);
+      float v = 0.f;
+      for (int k = 0; k < (K >> 8); ++k) {
+        const f4 x = r[k];
+        v = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(v, x.x), x.y), x.z), x.w);
+      }
+      res[2 * slot + lane] = v;
+    }
+    wave_lds_fence();  // the scratch is rewritten by the next slot
   }
 }
 
@@ -335,10 +354,18 @@ TL_DEVICE void load_any(const PDesc& d, const PGeo& g, const PStep& p, int slot,
   else load_slot(d, g, p, slot, lane, buf);
 }
 
+// int8 chain buffers of one wave: the products of rows longer than one chunk (pbuf, row stride
+// pgp) and the wave's own 2 x 68-float scratch (cw)
+struct PChain {
+  float* pbuf;
+  int pgp;
+  float* cw;
+};
+
 template <bool Q8>
-TL_DEVICE void consume_any(const PGeo& g, int slot, int lane, const f4 (&buf)[PL], const float (&sc)[PL],
-                           const f4* xs, const signed char* xq, const float* xsc, float* res) {
-  if constexpr (Q8) consume_slot_q8(g, slot, lane, buf, sc, xq, xsc, res);
+TL_DEVICE void consume_any(const PGeo& g, int K, int slot, int lane, const f4 (&buf)[PL], const float (&sc)[PL],
+                           const f4* xs, const signed char* xq, const float* xsc, float* res, const PChain& pc) {
+  if constexpr (Q8) consume_slot_q8(g, K, slot, lane, buf, sc, xq, xsc, res, pc.pbuf, pc.pgp, pc.cw);
   else consume_slot(g, slot, lane, buf, xs, res);
 }
 
@@ -359,7 +386,7 @@ TL_DEVICE int take_slot(unsigned* ctr, int lane) {
 template <bool Q8>
 TL_DEVICE void run_gemv(const PDesc& d, const PGeo& g, const PStep& p, int sw, int lane, const f4* xs,
                         const signed char* xq, const float* xsc, float* res, f4 (&buf)[NBUF][PL],
-                        float (&sc)[NBUF][PL], unsigned* ctr, unsigned long long* ts) {
+                        float (&sc)[NBUF][PL], unsigned* ctr, unsigned long long* ts, const PChain& pc) {
   int sl[NBUF];  // the slots the buffers hold (the phase's prefetch: sw, sw + NSW, ...)
 #pragma unroll
   for (int i = 0; i < NBUF; ++i) sl[i] = sw + i * NSW;
@@ -368,7 +395,7 @@ TL_DEVICE void run_gemv(const PDesc& d, const PGeo& g, const PStep& p, int sw, i
   while (sl[0] < g.nslot) {
 #pragma unroll
     for (int i = 0; i < NBUF; ++i) {
-      if (sl[i] < g.nslot) consume_any<Q8>(g, sl[i], lane, buf[i], sc[i], xs, xq, xsc, res);
+      if (sl[i] < g.nslot) consume_any<Q8>(g, d.K, sl[i], lane, buf[i], sc[i], xs, xq, xsc, res, pc);
       if (i == 0 && ts && first && lane == 0) *ts = __builtin_amdgcn_s_memrealtime();  // first slot landed
       first = false;
       __builtin_amdgcn_sched_barrier(0);
@@ -379,13 +406,20 @@ TL_DEVICE void run_gemv(const PDesc& d, const PGeo& g, const PStep& p, int sw, i
   }
 }
 
+// The reference's products x[j] * x[j] (runq.c:286) of float4 j into the seqsum layout.
+TL_DEVICE void put_squares(float* sqa, int ch, int j, f4 v) {
+  const int e = 4 * j;  // ch % 4 == 0: the four land in one chunk
+  float* d = sqa + seqsum_index(e, ch);
+  d[0] = __fmul_rn(v.x, v.x); d[1] = __fmul_rn(v.y, v.y); d[2] = __fmul_rn(v.z, v.z); d[3] = __fmul_rn(v.w, v.w);
+}
+
 // Granule sweep of the phase input into the LDS strip by threads t, t + T, ...: batches of NB
 // float4 (2*NB loads in flight per thread), then re-poll what was late.  sq: sum of squares.
 // UNC: unconditional (clamped) loads, so loads issued by `mid` after them keep the compiler's
 // vmcnt waits exact (int8, where mid issues slots); otherwise only threads with input load.
 template <int NB, bool UNC, class F>
 TL_DEVICE void gather(__amdgpu_buffer_rsrc_t r, unsigned tag, int n4, int pad4, int t, int T, f4* xs, float& sq,
-                      unsigned* err, F&& mid) {
+                      unsigned* err, float* sqa, int sqch, F&& mid) {
   for (int k0 = 0; k0 * T < pad4; k0 += NB) {
     v4u a[NB], b[NB];
 #pragma unroll
@@ -406,6 +440,7 @@ TL_DEVICE void gather(__amdgpu_buffer_rsrc_t r, unsigned tag, int n4, int pad4, 
           v = gran4_ok(a[k], b[k], tag) ? gran4_val(a[k], b[k]) : gran_wait4(r, (unsigned)j * 32u, tag, err);
         sq = fmaf(v.x, v.x, sq); sq = fmaf(v.y, v.y, sq); sq = fmaf(v.z, v.z, sq); sq = fmaf(v.w, v.w, sq);
         xs[j] = v;
+        if (sqa && j < n4) put_squares(sqa, sqch, j, v);
       }
     }
   }
@@ -462,7 +497,7 @@ TL_DEVICE void gather_q8(__amdgpu_buffer_rsrc_t r, unsigned tag, int n4, int nch
 // the token's embedding row (weights: plain loads).  Ends with a workgroup barrier.
 template <bool Q8, class F>
 TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, signed char* xq, float* xsc,
-                     const float* rmsw, float* red, int wave, int lane, unsigned long long* ts, F&& mid) {
+                     const float* rmsw, float* red, float* sqa, int wave, int lane, unsigned long long* ts, F&& mid) {
   const int n4 = d.K >> 2, pad4 = Q8 ? n4 : g.nch * PL * 64;
   if (Q8 && d.kind == PK_WO) {
     // the attention units published the Wo input already quantised (attention.hpp
@@ -501,6 +536,10 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, sign
     return;
   }
   float sq = 0.f;
+  // int8: the norm's sum of squares is runq's left-to-right chain (seqsum.hpp), so the squares
+  // go to the seqsum layout as they arrive
+  float* sqd = Q8 && d.rms ? sqa : nullptr;
+  const int sqch = d.K >> 6;  // seqsum_ch(K) for K % 256 == 0
   if (!d.gin) {
     mid();
     const f4* emb = reinterpret_cast<const f4*>(p.emb + (long long)p.tok[0] * p.dim);
@@ -508,30 +547,46 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, sign
       const f4 v = j < n4 ? emb[j] : f4{0.f, 0.f, 0.f, 0.f};
       sq = fmaf(v.x, v.x, sq); sq = fmaf(v.y, v.y, sq); sq = fmaf(v.z, v.z, sq); sq = fmaf(v.w, v.w, sq);
       xs[j] = v;
+      if (sqd && j < n4) put_squares(sqd, sqch, j, v);
     }
   } else {
     // every wave sweeps (the control wave alone, 16-24 loads in flight, was 1.4x slower per
     // step: the sweep is bound by loads in flight, not by the streaming waves' queued slots)
-    gather<SB, Q8>(rsrc_of(d.gin), d.tag_in, n4, pad4, threadIdx.x, PT, xs, sq, p.err, mid);
+    gather<SB, Q8>(rsrc_of(d.gin), d.tag_in, n4, pad4, threadIdx.x, PT, xs, sq, p.err, sqd, sqch, mid);
   }
   if (ts && lane == 0) ts[wave == 0 ? 8 : 10] = __builtin_amdgcn_s_memrealtime();  // input gathered
   float ss = 1.f;
   if (d.rms) {
-    // reference rmsnorm (src/seq.cpp:3-16): ss = 1/sqrtf(sum/size + 1e-5f); the block sum
-    // is taken in a fixed order (waves 0..PW-1), so every block gets the same ss
-    sq = wave_sum_u(sq);
-    if (lane == 0) red[wave] = sq;
-    __syncthreads();
-    float t = red[0];
+    // reference rmsnorm (src/seq.cpp:3-16, runq.c:282-295): ss = 1/sqrtf(sum/size + 1e-5f).
+    // fp32: the block sum in a fixed order (waves 0..PW-1), so every block gets the same ss;
+    // int8: the sum is runq's own chain, taken by wave 0 (seqsum.hpp), bit for bit
+    float t;
+    if constexpr (Q8) {
+      __syncthreads();  // the squares are in sqa
+      if (wave == 0) {
+        const float v = wave_seqsum(sqa, d.K, lane);
+        if (lane == 0) red[0] = v;
+      }
+      __syncthreads();
+      t = red[0];
+    } else {
+      sq = wave_sum_u(sq);
+      if (lane == 0) red[wave] = sq;
+      __syncthreads();
+      t = red[0];
 #pragma unroll
-    for (int w = 1; w < PW; ++w) t += red[w];
+      for (int w = 1; w < PW; ++w) t += red[w];
+    }
     ss = __fdiv_rn(1.0f, sqrtf(__fadd_rn(__fdiv_rn(t, (float)d.K), 1e-5f)));
     if constexpr (!Q8) {
       const f4* w4 = reinterpret_cast<const f4*>(rmsw);
       for (int j = threadIdx.x; j < n4; j += PT) xs[j] = rms_apply(xs[j], w4[j], ss);
     }
   }
-  if (ts && lane == 0 && wave == 0) ts[9] = __builtin_amdgcn_s_memrealtime();  // normalised
+  if (ts && lane == 0 && wave == 0) {
+    ts[9] = __builtin_amdgcn_s_memrealtime();  // normalised
+    ts[11] = ((unsigned long long)__float_as_uint(ss) << 32) | (d.rms ? __float_as_uint(red[0]) : 0u);  // diagnostics
+  }
   if constexpr (Q8) {
     // runq.c:145-171 quantize over the padded strip (the RMSNorm applied on the fly, same
     // arithmetic as the fp32 strip): 8 consecutive threads per group of 64, 8 values each;
@@ -579,14 +634,25 @@ TL_DEVICE float2 rope_cs(const PStep& p, int row) {
 // xres: this block's slice of the residual stream x (rows i0.. of the dim-row phases, the
 // same slice for Wo and W2), kept in LDS so the residual add never re-reads x.
 TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const float* res, float* xres, int lane,
-                        int l, float2 cs0) {
+                        int l, float2 cs0, const float* pbuf) {
   unsigned long long best = 0;
   for (int it = lane; it < g.ni; it += 64) {
     float v[2] = {0.f, 0.f};
     for (int r = 0; r < d.rpi; ++r) {
-      const float* rr = res + (it * d.rpi + r) * g.nch;
-      float s = rr[0];
-      for (int c = 1; c < g.nch; ++c) s = __fadd_rn(s, rr[c]);
+      float s;
+      if (p.q8 && g.nch > 1) {
+        // int8 rows longer than a chunk: runq's chain over the row's group products (runq.c:330-338)
+        const f4* pr = reinterpret_cast<const f4*>(pbuf + (it * d.rpi + r) * p.pgp);
+        s = 0.f;
+        for (int k = 0; k < (d.K >> 8); ++k) {
+          const f4 x = pr[k];
+          s = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(s, x.x), x.y), x.z), x.w);
+        }
+      } else {
+        const float* rr = res + (it * d.rpi + r) * g.nch;
+        s = rr[0];
+        for (int c = 1; c < g.nch; ++c) s = __fadd_rn(s, rr[c]);
+      }
       v[r] = s;
     }
     const int item = g.i0 + it;
@@ -669,7 +735,8 @@ TL_DEVICE void grid_barrier(const PStep& p) {
 // norm preloads); the other waves stream.  Both execute the same workgroup barriers.
 template <int HS, bool ROLE0, bool Q8>
 TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* res, float* xres, float* red,
-                      float* rmsw, f4* xs, signed char* xq, float* xsc, unsigned tb) {
+                      float* rmsw, f4* xs, signed char* xq, float* xsc, float* sqa, float* scr, float* cwb,
+                      unsigned tb) {
   const int G = gridDim.x;
   const int nph = 5 * p.L + 1;
   unsigned* ctr = reinterpret_cast<unsigned*>(red + 15);  // dynamic slot counter (red[0..PW) is the norm sum)
@@ -699,14 +766,19 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
         if (Q8) { aw.gq8 = p.gxq; aw.gq8s = p.gxs; }  // the Wo input leaves quantised
         aw.tag_in = tb + 5u * l + 1; aw.tag_out = tb + 5u * l + 2; aw.err = p.err;
         aw.ts = p.trace ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots + 8 : nullptr;
-        const int units = p.H * p.NS;
-        for (int u = blockIdx.x; u < units; u += G) attn_unit<HS, 16, true>(aw, u, strips, lane);
+        if constexpr (Q8) {
+          // int8: runq's attention bit for bit, one unit per head (attention.hpp attn_unit_exact)
+          for (int u = blockIdx.x; u < p.H; u += G) attn_unit_exact<HS, true>(aw, 0, u, scr, lane);
+        } else {
+          const int units = p.H * p.NS;
+          for (int u = blockIdx.x; u < units; u += G) attn_unit<HS, 16, true>(aw, u, strips, lane);
+        }
         TRACE(3);
         continue;
       }
       const PDesc d = make_desc<Q8>(p, kind, l, tb);
       const PGeo g = geo<Q8>(d);
-      stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, wave, lane,
+      stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, sqa, wave, lane,
                 p.trace ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots : nullptr, [] {});
       TRACE(1);
       float2 cs0 = make_float2(1.f, 0.f);
@@ -718,7 +790,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
       __syncthreads();  // every slot reduced into res
       if (lane == 0) *ctr = 0u;  // next GEMV phase's slot counter (used after its staging barrier)
       TRACE(2);
-      epilogue(d, g, p, res, xres, lane, l, cs0);
+      epilogue(d, g, p, res, xres, lane, l, cs0, scr);
       TRACE(3);
     }
   } else {
@@ -751,11 +823,12 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
 #pragma unroll
         for (int i = pfn<Q8>(); i < NBUF; ++i) load_any<Q8>(d, g, p, sw + i * NSW, lane, buf[i], sc[i]);
       };
-      stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, wave, lane,
+      stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, sqa, wave, lane,
                 tr ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots : nullptr, mid);
       if (tr) TRACE(4);
       run_gemv<Q8>(d, g, p, sw, lane, xs, xq, xsc, res, buf, sc, ctr,
-                   tr ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots + 5 : nullptr);
+                   tr ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots + 5 : nullptr,
+                   PChain{scr, p.pgp, cwb + sw * 136});
       if (tr) TRACE(6);
       // every slot reduced into res: the control wave's epilogue (the hand-off every other
       // block waits for) starts now, not after this wave's next-phase issue (measured +5%)
@@ -810,16 +883,21 @@ __global__ void __launch_bounds__(PT) persistent_step_kernel(PStep p) {
   f4* xs = reinterpret_cast<f4*>(rmsw + p.dim);     // pad_floats: the staged input
   signed char* xq = reinterpret_cast<signed char*>(rmsw + p.dim + p.pad_floats);  // Q8: q8_pad int8
   float* xsc = reinterpret_cast<float*>(xq + p.q8_pad);                           //     q8_pad/64 scales
+  // int8 only (exact arithmetic): the norm's squares (seqsum layout) | the long rows' group
+  // products, aliased with the attention unit's strip | the streaming waves' chain scratch
+  float* sqa = xsc + p.q8_pad / 64;
+  float* scr = sqa + p.n_sqa;
+  float* cwb = scr + p.n_scr;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const unsigned tb = p.seq[0] << 12;  // tag base of this launch
-  if (wave == 0) phases<HS, true, Q8>(p, wave, lane, strips, res, xres, red, rmsw, xs, xq, xsc, tb);
-  else phases<HS, false, Q8>(p, wave, lane, strips, res, xres, red, rmsw, xs, xq, xsc, tb);
+  if (wave == 0) phases<HS, true, Q8>(p, wave, lane, strips, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, tb);
+  else phases<HS, false, Q8>(p, wave, lane, strips, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, tb);
 }
 
 static size_t lds_bytes(const PStep& p) {
   return (size_t)(64 + kPResidFloats + kPResFloats + 16 + p.dim + p.pad_floats) * 4 + (size_t)p.q8_pad +
-         (size_t)p.q8_pad / 16;
+         (size_t)p.q8_pad / 16 + (size_t)(p.n_sqa + p.n_scr + p.n_cw) * 4;
 }
 
 template <int HS, bool Q8>
@@ -854,6 +932,30 @@ bool persistent_prepare(PStep& p, int ncu, const char** why) {
   };
   p.pad_floats = padf(p.dim) > padf(p.hid) ? padf(p.dim) : padf(p.hid);
   p.q8_pad = p.q8 ? 4096 * (nchunks(p.dim) > nchunks(p.hid) ? nchunks(p.dim) : nchunks(p.hid)) : 0;
+  p.n_sqa = p.n_scr = p.n_cw = p.pgp = 0;
+  if (p.q8) {
+    // the norm's squares: seqsum layout of dim values (ch = dim / 64, rows of ch + 4)
+    p.n_sqa = 64 * (p.dim / 64 + 4);
+    // group products of the rows longer than a chunk (row stride pgp), per phase
+    int rows_max = 0, gp = 0;
+    auto longrows = [&](int K, int n_items, int rpi) {
+      if (nchunks(K) < 2) return;
+      const int stride = nchunks(K) * 64 + 4;
+      const int rows = (int)((long long)n_items * (100 + kXcdSkew) / part_weight(ncu) + 2) * rpi;
+      gp = stride > gp ? stride : gp;
+      rows_max = rows > rows_max ? rows : rows_max;
+    };
+    longrows(p.dim, (p.dim + 2 * p.kvd) / 2, 2);
+    longrows(p.dim, p.dim, 1);
+    longrows(p.dim, p.hid, 2);
+    longrows(p.hid, p.dim, 1);
+    longrows(p.dim, p.V, 1);
+    p.pgp = gp;  // one stride for every long-row phase
+    const int pb = rows_max * gp;
+    const int attn = 3 * p.hs + 64 * (4 * ((p.S + 255) / 256) + 4) + ((p.S + 3) & ~3) + 64;  // attn_exact_floats
+    p.n_scr = ((pb > attn ? pb : attn) + 3) & ~3;
+    p.n_cw = NSW * 136;
+  }
   if (nrc(p.dim, (p.dim + 2 * p.kvd) / 2, 2) > kPResFloats || nrc(p.dim, p.hid, 2) > kPResFloats ||
       nrc(p.hid, p.dim, 1) > kPResFloats || nrc(p.dim, p.V, 1) > kPResFloats)
     return fail("too many rows per block");

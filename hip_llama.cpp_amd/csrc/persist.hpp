@@ -37,6 +37,9 @@ struct PStep {
   const signed char* qcls;
   const float* scls;
   int q8_pad;               // LDS bytes of the quantised activation strip (Q8 only)
+  int n_sqa, n_scr, n_cw;   // Q8 (exact arithmetic) LDS floats: norm squares, long-row products /
+                            // attention strip, streaming-wave chain scratch (persistent_prepare)
+  int pgp;                  // Q8: row stride (floats) of the long-row products
   int fault;                // test hook (THALLAMA_OPT_PERSIST_FAULT): block 0 exits at once, as
                             // if the grid were not co-resident; every other wait gives up
 };

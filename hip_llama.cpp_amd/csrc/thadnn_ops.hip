@@ -10,6 +10,7 @@
 #include "../../include/thaDNN.hpp"
 #include "../../include/hip_helper.hpp"
 #include "common.hpp"
+#include "libm_exact.hpp"
 
 using tl::f4;
 
@@ -97,7 +98,7 @@ extern "C" thablasStatus_t thaDNN_s_rope(thablasHandle_t* handle, int dim, int h
 // ------------------------------------------------------------------ SwiGLU
 // reference src/thaDNN/thaDNN_swiglu.cpp:5-14 ; CPU src/seq.cpp:159-166
 __device__ __forceinline__ float swiglu1(float a, float b) {
-  float s = __fdiv_rn(1.0f, __fadd_rn(1.0f, expf(-a)));
+  float s = __fdiv_rn(1.0f, __fadd_rn(1.0f, tl::expf_libm(-a)));
   return __fmul_rn(__fmul_rn(a, s), b);
 }
 
@@ -130,7 +131,7 @@ __global__ void __launch_bounds__(256) k_softmax_rows(float* x, long long stride
   m = tl::block_max(m, red);
   float s = 0.f;
   for (int i = threadIdx.x; i < size; i += 256) {
-    float e = expf(__fsub_rn(row[i], m));
+    float e = tl::expf_libm(__fsub_rn(row[i], m));
     row[i] = e;
     s += e;
   }

@@ -155,6 +155,7 @@ def lib():
             "thallama_decoder_set": (I, [VP, I, I]),
             "thallama_decoder_persistent": (I, [VP]),
             "thallama_persistent_cooperative": (I, []),
+            "thallama_decoder_granules": (I, [VP, C.POINTER(C.c_ulonglong), S]),
             "thallama_decoder_prefill": (I, [VP, I, c_int_p, I, I]),
             "thallama_decoder_ptrace": (I, [VP, I, C.POINTER(C.c_ulonglong), C.c_size_t]),
             "thallama_decoder_stream": (VP, [VP]),

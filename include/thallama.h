@@ -47,6 +47,10 @@ int thallama_decoder_persistent(thallama_decoder* d);
 /* 1 if the persistent step is dispatched as a cooperative launch (grid co-residency guaranteed
  * by the runtime), 0 for a plain launch (THALLAMA_PERSIST_COOP=0 or no device support). */
 int thallama_persistent_cooperative(void);
+/* Diagnostics: the persistent step's hand-off granules ({value, tag}: x | xb | hb | q k v | int8
+ * codes | scales; the last layer's after a launch) into host[n]; returns the count (host NULL:
+ * count only). */
+int thallama_decoder_granules(thallama_decoder* d, unsigned long long* host, size_t n);
 /* Diagnostics: enable != 0 allocates a timeline buffer that every later persistent launch
  * fills with 100-MHz clock stamps, [grid][5*n_layers+1][4] (phase start, input staged,
  * slots reduced, epilogue drained); host != NULL copies up to n stamps out (synchronous).

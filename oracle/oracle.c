@@ -231,6 +231,11 @@ float* oracle_model_logits(OModel* m) { return m->logits; }
 float* oracle_model_kcache(OModel* m) { return m->kc; }
 float* oracle_model_vcache(OModel* m) { return m->vc; }
 float* oracle_model_x(OModel* m) { return m->x; }
+/* RunState buffers after a forward (diagnostics): 0 x, 1 xb, 2 xb2, 3 hb, 4 hb2, 5 q, 6 k, 7 v */
+float* oracle_model_buf(OModel* m, int which) {
+  float* b[8] = {m->x, m->xb, m->xb2, m->hb, m->hb2, m->q, m->k, m->v};
+  return which >= 0 && which < 8 ? b[which] : NULL;
+}
 
 void oracle_model_reset_kv(OModel* m) {
   const OCfg* p = &m->c;

@@ -61,6 +61,7 @@ def lib():
             "oracle_model_kcache": (F, [V]),
             "oracle_model_vcache": (F, [V]),
             "oracle_model_x": (F, [V]),
+            "oracle_model_buf": (F, [V, C.c_int]),
             "oracle_model_reset_kv": (None, [V]),
             "oracle_write_v0": (C.c_int, [V, C.c_char_p]),
             "oracle_model_free": (None, [V]),
@@ -199,6 +200,10 @@ class Model:
         out = (C.c_int * n)()
         lib().oracle_greedy(self.h, token, pos0, n, out)
         return list(out)
+
+    def buf(self, which, n):
+        """RunState buffer after a forward: 0 x, 1 xb, 2 xb2, 3 hb, 4 hb2, 5 q, 6 k, 7 v (diagnostics)."""
+        return np.ctypeslib.as_array(lib().oracle_model_buf(self.h, which), shape=(n,)).copy()
 
     def reset_kv(self):
         lib().oracle_model_reset_kv(self.h)

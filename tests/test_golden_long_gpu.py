@@ -57,3 +57,48 @@ def test_fp32_256_step_greedy_equals_reference(gpu, name, path):
         assert_ref_close(lg[b], LAST[name + "_fp32_last"], 1e-4, f"{name} {path} seq {b} last-step logits")
         d = g["digests"][-1]
         assert int(np.argmax(lg[b])) == d["argmax"]
+
+
+def q8_decoder(tl, case, batch):
+    c = tl.Config.make(*case["config"])
+    m = tl.DeviceModel(c, case["shared"], seed=case["seed"])
+    q = tl.DeviceModelQ8(c, case["shared"], case["q8"]["group_size"], from_model=m)
+    state = tl.DeviceState(c, batch)
+    return (m, q, state), tl.Decoder(q, state)
+
+
+def f32bits_of(d):
+    return np.array(d, np.uint32).view(np.float32)
+
+
+@pytest.mark.parametrize("name", ["stories110m_shared", "stories110m_unshared", "llama2_7b"])
+def test_int8_256_step_greedy_bitexact_vs_runq(gpu, name):
+    """BASELINE configs[3]: the int8 (runq) greedy decode on the persistent step — every one of the
+    256 tokens equals runq's, and the last step's logits are bit-identical to runq's (the 110M
+    unshared case includes a step whose top-2 margin is 1.2e-6: only exact arithmetic holds it)."""
+    case = CASES[name]
+    g = case["q8"]
+    keep, dec = q8_decoder(gpu, case, 1)
+    dec.set(gpu.OPT_USE_GRAPH, 1)
+    assert dec.persistent()
+    got = dec.greedy([case["start_token"]], [case["start_pos"]], case["steps"])[:, 0].tolist()
+    first = next((i for i, (a, w) in enumerate(zip(got, g["tokens"])) if a != w), None)
+    assert first is None, (f"{name} int8: token {first} differs (got {got[first]}, runq {g['tokens'][first]}, "
+                           f"runq top-2 margin there {g['margins'][first]:.3g})")
+    lg = dec.logits()[0]
+    np.testing.assert_array_equal(lg.view(np.uint32), LAST[name + "_q8_last"].view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["stories110m_unshared", "llama2_7b"])
+def test_int8_teacher_forced_digests_bitexact(gpu, name):
+    """Along runq's own tokens, every step's logits digest (first 8 logits and the top-5 values as
+    float32 bits) equals runq's."""
+    case = CASES[name]
+    g = case["q8"]
+    keep, dec = q8_decoder(gpu, case, 1)
+    toks = [case["start_token"]] + g["tokens"][:-1]
+    for p, t in enumerate(toks):
+        lg = dec.forward([t], [p])[0]
+        d = g["digests"][p]
+        assert lg[:8].view(np.uint32).tolist() == d["head_bits"], f"{name} int8 pos {p} head"
+        assert lg[d["top5"]].view(np.uint32).tolist() == d["top5_bits"], f"{name} int8 pos {p} top-5"

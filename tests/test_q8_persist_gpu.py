@@ -95,3 +95,28 @@ def test_q8_persistent_repeated_launches(gpu, oracle):
     want = ref.q8_greedy(1, 0, 10)
     for _ in range(3):
         assert dec.greedy([1], [0], 10)[:, 0].tolist() == want
+
+
+@pytest.mark.parametrize("cfg,shared", [(SMALL, 0), (HEAD128, 0), (RAGGED, 0), (WIDE, 0), (HEAD64_GQA, 0),
+                                        (SMALL, 1)])
+def test_q8_persistent_bitexact_vs_runq(gpu, oracle, cfg, shared):
+    """The persistent int8 step computes runq's arithmetic in runq's order (group products chained
+    left to right, runq.c:330-338; the norm's sum of squares and the softmax denominator as
+    left-to-right chains, seqsum.hpp; attention one key / column per lane in the reference's
+    order; the host libm's expf, libm_exact.hpp): teacher-forced logits are BIT-IDENTICAL to
+    runq's (the oracle restatement, pinned to runq.c in tests/test_oracle.py), at every step up
+    to 3 x 64 + 5 positions (several attention rounds)."""
+    oracle.set_threads(16)
+    _, keep, _, dec = q8_decoder(gpu, cfg, shared, 31, 1)
+    assert dec.persistent()
+    ref = oracle.Model(cfg, shared, seed=31)
+    ref.build_q8(64)
+    n = min(cfg[6], 197)
+    toks = np.random.default_rng(5).integers(0, cfg[5], n)
+    for p, t in enumerate(toks):
+        got = dec.forward([int(t)], [p])[0]
+        want = ref.q8_forward(int(t), p)
+        if not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
+            bad = np.flatnonzero(got.view(np.uint32) != want.view(np.uint32))
+            raise AssertionError(f"pos {p}: {bad.size} logits differ (first {bad[0]}: {got[bad[0]]!r} vs "
+                                 f"{want[bad[0]]!r}, max |d| {np.max(np.abs(got - want)):.3g})")
