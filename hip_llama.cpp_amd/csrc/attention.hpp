@@ -147,9 +147,9 @@ struct AttnWaveParams {
   unsigned tag_in, tag_out;
   unsigned* err;
   unsigned long long* ts;          // optional timeline (persistent step trace): q ready, k/v ready, done
-  // int8 weights (persistent step): the output leaves quantised instead (publish_head):
-  // {4 codes, tag} granules [dim/4] and {group scale, tag} granules [dim/64]; null: fp32 gout
-  unsigned long long *gq8, *gq8s;
+  // int8 weights (persistent step, attn_unit_split): the score granules [H][seq_len]
+  unsigned long long* gsc;
+  const uint64_t* etab;  // the expf table (libm_exact.hpp), an LDS copy
   // int8 weights, multi-launch batched step: the output row is also stored quantised (codes
   // [b][dim], group scales [b][dim/64]) so the Wo launch that follows needs no quantise pass
   signed char* xq8;
@@ -216,42 +216,22 @@ TL_DEVICE void store_head(const AttnWaveParams& w, int b, int h, const float* v,
   if (lane < VPL) w.xq8s[(long long)b * (p.dim / 64) + h * VPL + lane] = lsc;
 }
 
-// Persistent step: publish head h's output row (lane holds columns lane*VPL + c).  fp32
-// weights: one {value, tag} granule per value.  int8 weights (w.gq8 set): runq's activation
-// quantisation of the row's 64-value groups happens here (runq.c:145-171; the arithmetic of
-// the staging's q8_pack on the same floats, so the codes are the ones the Wo phase computed
-// itself before) and the row leaves as {4 codes, tag} and {scale, tag} granules: the Wo
-// phase gathers a quarter of the bytes and quantises nothing.  `strip`: the wave's LDS strip
-// (>= HS bytes).  All 64 lanes active.
+// Persistent step (fp32 weights): publish head h's output row (lane holds columns lane*VPL + c)
+// as {value, tag} granules.
 template <int HS>
-TL_DEVICE void publish_head(const AttnWaveParams& w, int h, const float* v, float* strip, int lane) {
+TL_DEVICE void publish_head(const AttnWaveParams& w, int h, const float* v, int lane) {
   constexpr int VPL = HS / 64;
-  if (!w.gq8) {
 #pragma unroll
-    for (int c = 0; c < VPL; ++c) st8_sc1(w.gout + h * HS + lane * VPL + c, gran(w.tag_out, v[c]));
-    return;
-  }
-  float lsc;
-  const unsigned packed = head_q8<HS>(v, lane, lsc);
-  // VPL codes per lane -> dwords of 4 codes through the strip
-  unsigned char* sb = reinterpret_cast<unsigned char*>(strip);
-  if constexpr (VPL == 1) sb[lane] = (unsigned char)packed;
-  else if constexpr (VPL == 2) reinterpret_cast<unsigned short*>(sb)[lane] = (unsigned short)packed;
-  else reinterpret_cast<unsigned*>(sb)[lane] = packed;
-  wave_lds_fence();
-  if (lane < HS / 4)
-    st8_sc1(w.gq8 + h * (HS / 4) + lane, gran(w.tag_out, __uint_as_float(reinterpret_cast<const unsigned*>(sb)[lane])));
-  if (lane < VPL) st8_sc1(w.gq8s + h * VPL + lane, gran(w.tag_out, lsc));
-  wave_lds_fence();  // the strip is rewritten by the next unit
+  for (int c = 0; c < VPL; ++c) st8_sc1(w.gout + h * HS + lane * VPL + c, gran(w.tag_out, v[c]));
 }
 
-// The body of one attention unit, run by one full wave.  `sc` (a 64-float LDS strip) is used
-// only by publish_head's int8 output; `unit` must be wave-uniform.  Also used inside the persistent step
+// The body of one attention unit, run by one full wave; `unit` must be wave-uniform.  Also used
+// inside the persistent step
 // kernel (persist.hip) with GR = true: q and the K/V rows at position pos come from the
 // granules the QKV phase of the same launch published (rows < pos were written by earlier
 // launches and are read from the cache), and the output is published as granules.
 template <int HS, int CH, bool GR = false>
-TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane) {
+TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
   constexpr int LPK = HS / 4;    // lanes per key row (one float4 each)
   constexpr int KPI = 64 / LPK;  // keys per wave-instruction
   constexpr int NI = CH / KPI;   // K wave-loads per chunk
@@ -413,7 +393,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane)
   if (whole) {
     if constexpr (GR) {
       if (w.ts && lane == 0) w.ts[2] = __builtin_amdgcn_s_memrealtime();
-      publish_head<HS>(w, h, o, sc, lane);
+      publish_head<HS>(w, h, o, lane);
     } else {
       store_head<HS>(w, b, h, o, lane);
     }
@@ -462,7 +442,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane)
 #pragma unroll
   for (int c = 0; c < VPL; ++c) acc[c] = __fdiv_rn(acc[c], L);
   if constexpr (GR) {
-    publish_head<HS>(w, h, acc, sc, lane);
+    publish_head<HS>(w, h, acc, lane);
   } else {
     store_head<HS>(w, b, h, acc, lane);
   }
@@ -472,138 +452,183 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, float* sc, int lane)
 // Stand-alone launch: one 64-thread block per unit.
 template <int HS, int CH>
 __global__ void __launch_bounds__(64) attn_wave_kernel(AttnWaveParams w) {
-  __shared__ float sc[64];
-  attn_unit<HS, CH>(w, blockIdx.x, sc, threadIdx.x);
+  attn_unit<HS, CH>(w, blockIdx.x, threadIdx.x);
 }
 
 // ---------------------------------------------------------------------------
 // runq's attention, bit for bit (runq.c:396-434; the same order as src/seq.cpp:103-136), for the
-// int8 path: the Wo input is re-quantised, so the head output must be the reference's floats.
+// int8 persistent step: the Wo input is re-quantised, so the head output must be the reference's
+// floats.
 //   score_t = (((0 + q0 k0) + q1 k1) + ...) / sqrtf(hs)      one lane per key, sequential dot
 //   e_t = expf(score_t - max);  sum = e_0 + e_1 + ...         libm_exact.hpp; seqsum.hpp
 //   a_t = e_t / sum;  xb_i = ((0 + a_0 v0_i) + a_1 v1_i) + ...  one lane per output column
-// One full wave per (sequence b, head h).  `strip` (LDS) holds attn_exact_floats(hs, T) floats.
-// GR (persistent step): q and this step's k/v rows come from the granules.  Products and sums
-// are single roundings (no contraction), like the reference compiled without FMA.
-TL_DEVICE int attn_exact_floats(int hs, int T) { return 3 * hs + seqsum_floats(T) + ((T + 3) & ~3) + 64; }
+// Every score and every column is independent; only the sum and the column chains are ordered.
+// So a head is split over NG units (blocks) c = 0..NG-1: unit c scores keys [T c/NG, T (c+1)/NG)
+// and publishes them as {score, tag} granules (gsc, [H][S]); every unit of the head gathers all T
+// scores, repeats the softmax (max, expf, the exact sum: identical in every unit) and chains its
+// HS/NG columns over all T rows; the columns leave as fp32 {value, tag} granules (gout) and the
+// Wo phase quantises them while it gathers (runq.c:145-171, persist.hip gather_q8).
+// Memory: a unit's K slice (<= 64 keys a round) and V column slice (rows of HS/NG floats) reach
+// LDS by LDS-DMA (global_load_lds: no registers), all requested at the unit's start — before q
+// has arrived — so the whole head costs about one memory latency instead of one per 64 keys.
+// q and this step's k/v rows come from the QKV phase's granules.  Products and sums are single
+// roundings (the library is built with -ffp-contract=off).
+// LDS: `strip` holds attn_split_floats(hs, T) floats; `win` (nwin floats) holds a K round
+// (64 keys transposed: piece i of key l at win[i*256 + 4l], so lane l reads its key
+// conflict-free) followed by the V rows [rows][HS/NG].
+TL_DEVICE int attn_split_floats(int hs, int T) { return 3 * hs + seqsum_floats(T) + ((T + 3) & ~3) + 64; }
 
-template <int HS, bool GR>
-TL_DEVICE void attn_unit_exact(const AttnWaveParams& w, int b, int h, float* strip, int lane) {
+TL_DEVICE void dma16(const float* src, float* dst_lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)dst_lds, 16, 0, 0);
+}
+TL_DEVICE void dma_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+template <int HS>
+TL_DEVICE void attn_unit_split(const AttnWaveParams& w, int h, int c, int NG, float* strip, float* win, int nwin,
+                               int lane) {
   constexpr int VPL = HS / 64;
+  constexpr int PC = HS / 4;  // 16-byte pieces per key row
   const AttnParams& p = w.a;
-  const int T = p.pos[b] + 1;
+  const int T = p.pos[0] + 1;
+  const int tc = T - 1;  // rows read from the cache (row T-1 is this step's, from the granules)
   const int kvh = h / p.kv_mul;
-  const float* kbase = p.kc + (long long)b * p.kv_b_stride + p.kv_l_off + (long long)kvh * HS;
-  const float* vbase = p.vc + (long long)b * p.kv_b_stride + p.kv_l_off + (long long)kvh * HS;
-  float* qs = strip;             // q [HS]
-  float* kn = qs + HS;           // k row of position T-1 [HS] (granule mode)
-  float* vn = kn + HS;           // v row of position T-1 [HS]
-  float* sa = vn + HS;           // exp values, seqsum layout
-  float* at = sa + seqsum_floats(T);  // probabilities [T]
+  const float* kbase = p.kc + p.kv_l_off + (long long)kvh * HS;
+  const float* vbase = p.vc + p.kv_l_off + (long long)kvh * HS;
+  const int CW = HS / NG;           // this unit's columns
+  const int col0 = c * CW;
+  const int PPR = CW / 4;           // 16-byte pieces per V row slice
+  const int RPI = 64 / PPR;         // V rows per DMA instruction (1 KiB)
+  const int k0 = (int)((long long)T * c / NG), k1 = (int)((long long)T * (c + 1) / NG);
+  const int kc1 = min(k1, tc);      // cached keys of this unit: [k0, kc1)
+  float* qs = strip;                // q [HS]
+  float* kn = qs + HS;              // k row of position T-1 [HS]
+  float* vn = kn + HS;              // v row of position T-1 [HS]
+  float* sa = vn + HS;              // exp values, seqsum layout
+  float* at = sa + seqsum_floats(T);  // scores, then probabilities [T]
   const int ch = seqsum_ch(T);
+  float* vw = win + 64 * HS;        // V rows [rv][CW]
+  const int rq = RPI > 4 ? RPI : 4;
+  const int rv = (nwin - 64 * HS) / CW / rq * rq;  // V rows per round (host: >= 64; a multiple of 4)
+  unsigned long long* gs = w.gsc + (long long)h * p.seq_len;
+  // q / k_new / v_new granules first (their wait then does not cover the DMA behind them)
+  const unsigned long long* src[3] = {w.gqkv + h * HS, w.gqkv + p.dim + kvh * HS,
+                                      w.gqkv + p.dim + p.kv_dim + kvh * HS};
+  float* dst[3] = {qs, kn, vn};
+  unsigned long long g[3][VPL];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int cc = 0; cc < VPL; ++cc) g[r][cc] = ld8_sc1(src[r] + lane * VPL + cc);
+  auto issue_keys = [&](int t0) {  // keys t0 + lane (< kc1), transposed into win
+    if (t0 + lane < kc1) {
+      const float* row = kbase + (long long)(t0 + lane) * p.kv_dim;
+#pragma unroll
+      for (int i = 0; i < PC; ++i) dma16(row + 4 * i, win + i * 256);
+    }
+  };
+  auto issue_rows = [&](int r0, int n) {  // V rows [r0, r0 + n) of this unit's columns into vw
+    for (int k = 0; k * RPI < n; ++k) {
+      const int rr = k * RPI + lane / PPR;
+      if (rr < n) dma16(vbase + (long long)(r0 + rr) * p.kv_dim + col0 + (lane % PPR) * 4, vw + k * 256);
+    }
+  };
+  if (k0 < kc1) issue_keys(k0);
+  if (tc > 0) issue_rows(0, min(rv, tc));
   for (int i = lane; i < seqsum_floats(T); i += 64) sa[i] = 0.f;
-  if constexpr (GR) {
-    // q, k_new, v_new requested together (one round trip), late granules re-polled singly
-    const unsigned long long* src[3] = {w.gqkv + h * HS, w.gqkv + p.dim + kvh * HS,
-                                        w.gqkv + p.dim + p.kv_dim + kvh * HS};
-    float* dst[3] = {qs, kn, vn};
-    unsigned long long g[3][VPL];
 #pragma unroll
-    for (int r = 0; r < 3; ++r)
+  for (int r = 0; r < 3; ++r)
 #pragma unroll
-      for (int c = 0; c < VPL; ++c) g[r][c] = ld8_sc1(src[r] + lane * VPL + c);
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-      for (int c = 0; c < VPL; ++c)
-        dst[r][lane * VPL + c] = (unsigned)(g[r][c] >> 32) == w.tag_in
-                                     ? __uint_as_float((unsigned)g[r][c])
-                                     : gran_wait(src[r] + lane * VPL + c, w.tag_in, w.err);
-    if (w.ts && lane == 0) w.ts[0] = __builtin_amdgcn_s_memrealtime();
-  } else {
-    const float* q = p.q + (long long)b * p.dim + h * HS;
-#pragma unroll
-    for (int c = 0; c < VPL; ++c) qs[lane * VPL + c] = q[lane * VPL + c];
-  }
+    for (int cc = 0; cc < VPL; ++cc)
+      dst[r][lane * VPL + cc] = (unsigned)(g[r][cc] >> 32) == w.tag_in
+                                    ? __uint_as_float((unsigned)g[r][cc])
+                                    : gran_wait(src[r] + lane * VPL + cc, w.tag_in, w.err);
+  if (w.ts && lane == 0) w.ts[0] = __builtin_amdgcn_s_memrealtime();
   wave_lds_fence();
-  // scores: lane t, t + 64, ... (cached rows; in granule mode row T-1 from the strip)
-  const float rs = sqrtf((float)HS);
-  float mx = -__builtin_inff();
-  for (int t0 = 0; t0 < T; t0 += 64) {
-    const int t = t0 + lane;
-    const int tl = t < T ? t : T - 1;
-    const bool fresh = GR && tl == T - 1;
-    const f4* kr = reinterpret_cast<const f4*>(kbase + (long long)(GR && tl == T - 1 ? (T >= 2 ? T - 2 : 0) : tl) * p.kv_dim);
-    const f4* k2 = reinterpret_cast<const f4*>(kn);
-    const f4* q4 = reinterpret_cast<const f4*>(qs);
+  const f4* q4 = reinterpret_cast<const f4*>(qs);
+  // sequential dot of q with the HS floats at base + i*stride4*4 (piece i); the pieces are read
+  // RA at a time ahead of the chain (an LDS read's latency per step otherwise)
+  constexpr int RA = 8;
+  auto dot_lds = [&](const float* base, int stride4) {
     float sc = 0.f;
-#pragma unroll 4
-    for (int i = 0; i < HS / 4; ++i) {
-      f4 kv = kr[i];
-      if (fresh) kv = k2[i];
-      const f4 qv = q4[i];
-      sc = __fadd_rn(sc, __fmul_rn(qv.x, kv.x));
-      sc = __fadd_rn(sc, __fmul_rn(qv.y, kv.y));
-      sc = __fadd_rn(sc, __fmul_rn(qv.z, kv.z));
-      sc = __fadd_rn(sc, __fmul_rn(qv.w, kv.w));
+    for (int i0 = 0; i0 < PC; i0 += RA) {
+      f4 k4[RA], qv[RA];
+#pragma unroll
+      for (int i = 0; i < RA; ++i) {
+        k4[i] = reinterpret_cast<const f4*>(base)[(i0 + i) * stride4];
+        qv[i] = q4[i0 + i];
+      }
+#pragma unroll
+      for (int i = 0; i < RA; ++i) {
+        sc = __fadd_rn(sc, __fmul_rn(qv[i].x, k4[i].x));
+        sc = __fadd_rn(sc, __fmul_rn(qv[i].y, k4[i].y));
+        sc = __fadd_rn(sc, __fmul_rn(qv[i].z, k4[i].z));
+        sc = __fadd_rn(sc, __fmul_rn(qv[i].w, k4[i].w));
+      }
     }
-    sc = __fdiv_rn(sc, rs);
-    if (t < T) {
-      at[t] = sc;
-      mx = fmaxf(mx, sc);
-    }
+    return sc;
+  };
+  // this unit's scores, published as granules
+  const float rs = sqrtf((float)HS);
+  for (int t0 = k0; t0 < kc1; t0 += 64) {
+    if (t0 > k0) issue_keys(t0);  // rounds past the first (contexts over 64 NG keys)
+    dma_wait_all();
+    const float sc = __fdiv_rn(dot_lds(win + 4 * lane, 64), rs);
+    if (t0 + lane < kc1) st8_sc1(gs + t0 + lane, gran(w.tag_out, sc));
+    wave_lds_fence();  // the window's reads are done before the next round lands in it
   }
+  if (k1 == T && lane == 0) st8_sc1(gs + T - 1, gran(w.tag_out, __fdiv_rn(dot_lds(kn, 1), rs)));
+  // every score of the head (the other units' granules)
+  float mx = -__builtin_inff();
+  for (int t = lane; t < T; t += 64) {
+    const unsigned long long x = ld8_sc1(gs + t);
+    const float sc = (unsigned)(x >> 32) == w.tag_out ? __uint_as_float((unsigned)x) : gran_wait(gs + t, w.tag_out, w.err);
+    at[t] = sc;
+    mx = fmaxf(mx, sc);
+  }
+  if (w.ts && lane == 0) w.ts[1] = __builtin_amdgcn_s_memrealtime();
   mx = wave_max_u(mx);  // exact (a maximum)
   wave_lds_fence();
-  for (int t = lane; t < T; t += 64) sa[seqsum_index(t, ch)] = expf_libm(__fsub_rn(at[t], mx));
+  for (int t = lane; t < T; t += 64) sa[seqsum_index(t, ch)] = expf_libm_tab(__fsub_rn(at[t], mx), w.etab);
   wave_lds_fence();
-  const float sum = wave_seqsum(sa, T, lane);
+  const float sum = T <= 512 ? wave_seqsum_short(sa, T) : T <= 4096 ? wave_seqsum_reg(sa, T, lane) : wave_seqsum(sa, T, lane);
+  if (w.ts && lane == 0) w.ts[3] = __builtin_amdgcn_s_memrealtime();
   for (int t = lane; t < T; t += 64) at[t] = __fdiv_rn(sa[seqsum_index(t, ch)], sum);
   wave_lds_fence();
-  // weighted sum of V: lane owns columns lane*VPL + c, a chain over t each
-  float o[VPL];
-#pragma unroll
-  for (int c = 0; c < VPL; ++c) o[c] = 0.f;
-  const int tc = GR ? T - 1 : T;  // rows read from the cache
-  int t = 0;
-  for (; t + 4 <= tc; t += 4) {
-    float vv[4][VPL];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int c = 0; c < VPL; ++c) vv[u][c] = vbase[(long long)(t + u) * p.kv_dim + lane * VPL + c];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const float a = at[t + u];
-#pragma unroll
-      for (int c = 0; c < VPL; ++c) o[c] = __fadd_rn(o[c], __fmul_rn(a, vv[u][c]));
+  // this unit's columns: lane < CW owns column col0 + lane, a chain over t
+  float o = 0.f;
+  const int cl = lane < CW ? lane : 0;
+  for (int r0 = 0; r0 < tc; r0 += rv) {
+    const int n = min(rv, tc - r0);
+    if (r0 > 0) {
+      wave_lds_fence();  // the previous round's reads are done
+      issue_rows(r0, n);
     }
-  }
-  for (; t < tc; ++t) {
-    const float a = at[t];
+    dma_wait_all();
+    // batches of 16 rows: all their LDS reads issued, then chained (the compiler waits for every
+    // LDS read before the first use, so a read-ahead across batches would not overlap)
+    const int n4 = n & ~15;
+    for (int u = 0; u < n4; u += 16) {
+      f4 a4[4];
+      float v16[16];
 #pragma unroll
-    for (int c = 0; c < VPL; ++c) o[c] = __fadd_rn(o[c], __fmul_rn(a, vbase[(long long)t * p.kv_dim + lane * VPL + c]));
-  }
-  if constexpr (GR) {
-    const float a = at[T - 1];
+      for (int k = 0; k < 4; ++k) a4[k] = *reinterpret_cast<const f4*>(at + r0 + u + 4 * k);
 #pragma unroll
-    for (int c = 0; c < VPL; ++c) o[c] = __fadd_rn(o[c], __fmul_rn(a, vn[lane * VPL + c]));
-    if (w.ts && lane == 0) w.ts[2] = __builtin_amdgcn_s_memrealtime();
-    wave_lds_fence();
-    publish_head<HS>(w, h, o, strip, lane);  // (the strip's q is dead)
-  } else {
-    store_head<HS>(w, b, h, o, lane);
+      for (int k = 0; k < 16; ++k) v16[k] = vw[(u + k) * CW + cl];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        o = __fadd_rn(o, __fmul_rn(a4[k].x, v16[4 * k]));
+        o = __fadd_rn(o, __fmul_rn(a4[k].y, v16[4 * k + 1]));
+        o = __fadd_rn(o, __fmul_rn(a4[k].z, v16[4 * k + 2]));
+        o = __fadd_rn(o, __fmul_rn(a4[k].w, v16[4 * k + 3]));
+      }
+    }
+    for (int u = n4; u < n; ++u) o = __fadd_rn(o, __fmul_rn(at[r0 + u], vw[u * CW + cl]));
   }
-  wave_lds_fence();
-}
-
-// Stand-alone launch of the exact unit (int8 multi-launch steps): one 64-thread block per
-// (sequence, head), grid B*H, dynamic LDS attn_exact_floats(HS, max T) floats.
-template <int HS>
-__global__ void __launch_bounds__(64) attn_exact_kernel(AttnWaveParams w) {
-  extern __shared__ __attribute__((aligned(16))) float strip[];
-  const int b = blockIdx.x / w.a.n_heads, h = blockIdx.x % w.a.n_heads;
-  attn_unit_exact<HS, false>(w, b, h, strip, threadIdx.x);
+  o = __fadd_rn(o, __fmul_rn(at[T - 1], vn[col0 + cl]));
+  if (w.ts && lane == 0) w.ts[2] = __builtin_amdgcn_s_memrealtime();
+  if (lane < CW) st8_sc1(w.gout + h * HS + col0 + lane, gran(w.tag_out, o));
+  wave_lds_fence();  // the strip and window are rewritten by the next unit
 }
 
 // out[b][h*hs + i] = sum_s o_s[i] e^{m_s-M} / sum_s l_s e^{m_s-M}

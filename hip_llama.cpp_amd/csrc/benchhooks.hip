@@ -136,3 +136,27 @@ extern "C" int thallama_seqsum_check(const float* in_d, int n, int count, float*
   if (e == hipSuccess) e = hipDeviceSynchronize();
   return (int)e;
 }
+
+// timing of the register form (clock cycles of one call per wave into cyc[count])
+__global__ void __launch_bounds__(64) k_seqsum_time(const float* in, int n, float* out, long long* cyc) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const float* a = in + (size_t)blockIdx.x * n;
+  const int ch = tl::seqsum_ch(n);
+  for (int i = threadIdx.x; i < tl::seqsum_floats(n); i += 64) lds[i] = 0.f;
+  __syncthreads();
+  for (int e = threadIdx.x; e < n; e += 64) lds[tl::seqsum_index(e, ch)] = a[e];
+  __syncthreads();
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  const float s = tl::wave_seqsum_reg(lds, n, threadIdx.x);
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) { out[blockIdx.x] = s; cyc[blockIdx.x] = t1 - t0; }
+}
+
+extern "C" int thallama_seqsum_time(const float* in_d, int n, int count, float* out_d, long long* cyc_d) {
+  if (!in_d || !out_d || !cyc_d || n <= 0 || n > 4096 || count <= 0) return (int)hipErrorInvalidValue;
+  const size_t lds = sizeof(float) * 64 * (4 * ((n + 255) / 256) + 4);
+  hipLaunchKernelGGL(k_seqsum_time, dim3(count), dim3(64), lds, 0, in_d, n, out_d, cyc_d);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  return (int)e;
+}

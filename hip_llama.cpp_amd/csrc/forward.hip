@@ -287,6 +287,7 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
   if (batch == 1) {
     tl::PStep ps = {};
     ps.dim = d->dim; ps.hid = d->hidden; ps.kvd = d->kv_dim; ps.hs = d->hs; ps.NS = d->nsplit;
+    ps.L = d->L; ps.H = d->H; ps.S = d->S; ps.V = d->V;
     const char* why = nullptr;
     d->pok = tl::persistent_prepare(ps, d->ncu, &why);
     if (!d->pok && why) d->pwhy = why;
@@ -298,8 +299,8 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
     TL_TRY(hipMalloc(&d->psync, sizeof(unsigned) * (d->psync_zero + 32)));
     TL_TRY(hipMemset(d->psync, 0, sizeof(unsigned) * (d->psync_zero + 32)));
     TL_TRY(hipMalloc(&d->pbmax, sizeof(unsigned long long) * d->ncu));
-    // x | xb | hb | qkv | int8 attention output codes (dim/4) and scales (dim/64)
-    const size_t ng = (size_t)3 * d->dim + d->hidden + 2 * d->kv_dim + d->dim / 4 + d->dim / 64 + 2;
+    // x | xb | hb | qkv | int8 attention scores [H][S]
+    const size_t ng = (size_t)3 * d->dim + d->hidden + 2 * d->kv_dim + (size_t)d->H * d->S + 2;
     TL_TRY(hipMalloc(&d->pgran, sizeof(unsigned long long) * ng));
     TL_TRY(hipMemset(d->pgran, 0, sizeof(unsigned long long) * ng));
   }
@@ -612,7 +613,7 @@ static int enqueue_persistent(thallama_decoder* d, bool argmax) {
   p.part = d->part_d; p.rope = d->rope_d;
   p.tok = d->tok_d; p.pos = d->pos_d; p.out = d->out_d;
   p.gx = d->pgran; p.gxb = p.gx + d->dim; p.ghb = p.gxb + d->dim; p.gqkv = p.ghb + d->hidden;
-  p.gxq = p.gqkv + d->dim + 2 * d->kv_dim; p.gxs = p.gxq + d->dim / 4;
+  p.gsc = p.gqkv + d->dim + 2 * d->kv_dim;
   p.sync = d->psync; p.tickets = d->psync + tl::kPSyncWords;
   p.err = d->psync + d->psync_zero; p.seq = p.err + 1; p.bmax = d->pbmax;
   p.argmax = argmax ? 1 : 0;
@@ -999,6 +1000,7 @@ extern "C" int thallama_decoder_create_q8(thallama_decoder** out, const Config* 
   if (d->pok) {
     tl::PStep ps = {};
     ps.dim = d->dim; ps.hid = d->hidden; ps.kvd = d->kv_dim; ps.hs = d->hs; ps.NS = d->nsplit; ps.L = d->L;
+    ps.H = d->H; ps.S = d->S; ps.V = d->V;
     ps.q8 = w8->group_size;
     const char* why = nullptr;
     d->pok = tl::persistent_prepare(ps, d->ncu, &why);

@@ -98,11 +98,15 @@ inline int mfma_target_blocks() {
   return v;
 }
 
-TL_DEVICE float silu_mul(float a, float b) {
+TL_DEVICE float silu_mul_tab(float a, float b, const uint64_t* etab) {
   // reference src/seq.cpp:159-166 / runq.c:455-462: val *= 1/(1+expf(-val)); val *= hb2, with
-  // the host libm's expf bit for bit (libm_exact.hpp)
-  float s = __fdiv_rn(1.0f, __fadd_rn(1.0f, expf_libm(-a)));
+  // the host libm's expf bit for bit (libm_exact.hpp; etab: its table, e.g. an LDS copy)
+  float s = __fdiv_rn(1.0f, __fadd_rn(1.0f, expf_libm_tab(-a, etab)));
   return __fmul_rn(__fmul_rn(a, s), b);
+}
+TL_DEVICE float silu_mul(float a, float b) {
+  constexpr uint64_t T[32] = TL_EXPF_TABLE;
+  return silu_mul_tab(a, b, T);
 }
 
 // Stage x'[b][kc .. kc+kcn) into LDS as NB rows of kcn floats.  When the whole

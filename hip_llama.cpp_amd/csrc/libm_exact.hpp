@@ -62,14 +62,11 @@ TL_LIBM_HD inline uint32_t libm_asu32(float f) {
 // fma(a, b, c) with one rounding, on both sides
 TL_LIBM_HD inline double libm_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
-TL_LIBM_HD inline float expf_libm(float x) {
+// T: the table above (expf_libm passes the constant; a kernel may pass a copy in LDS, which a
+// lane reads without a memory round trip)
+TL_LIBM_HD inline float expf_libm_tab(float x, const uint64_t* T) {
 #if defined(__clang__)
 #pragma clang fp contract(off)  // only the explicit fma below fuse (HIP compiles with contraction on)
-#endif
-#if defined(__HIP_DEVICE_COMPILE__)
-  constexpr uint64_t T[32] = TL_EXPF_TABLE;
-#else
-  static const uint64_t T[32] = TL_EXPF_TABLE;
 #endif
   const double InvLn2N = 0x1.71547652b82fep+0 * 32;
   const double Shift = 0x1.8p+52;
@@ -98,6 +95,15 @@ TL_LIBM_HD inline float expf_libm(float x) {
   y = libm_fma(z, r2, y);
   y = y * s;
   return (float)y;
+}
+
+TL_LIBM_HD inline float expf_libm(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  constexpr uint64_t T[32] = TL_EXPF_TABLE;
+#else
+  static const uint64_t T[32] = TL_EXPF_TABLE;
+#endif
+  return expf_libm_tab(x, T);
 }
 
 }  // namespace tl

@@ -332,13 +332,7 @@ TL_DEVICE void consume_slot_q8(const PGeo& g, int K, int slot, int lane, const f
   if (g.nch == 1) {
     wave_lds_fence();
     if (lane < 2 && 2 * slot + lane < g.nres) {
-      const f4* r = reinterpret_cast<const f4*>(cw + lane * 68);
-      float v = 0.f;
-      for (int k = 0; k < (K >> 8); ++k) {
-        const f4 x = r[k];
-        v = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(v, x.x), x.y), x.z), x.w);
-      }
-      res[2 * slot + lane] = v;
+      res[2 * slot + lane] = chain_f4(reinterpret_cast<const f4*>(cw + lane * 68), K >> 8, 0.f);
     }
     wave_lds_fence();  // the scratch is rewritten by the next slot
   }
@@ -495,40 +489,11 @@ TL_DEVICE void gather_q8(__amdgpu_buffer_rsrc_t r, unsigned tag, int n4, int nch
 // The input is the previous phase's granules (all issued at once, then re-polled until
 // their tags match), or — QKV at layer 0, or the classifier of a model without layers —
 // the token's embedding row (weights: plain loads).  Ends with a workgroup barrier.
-template <bool Q8, class F>
+template <bool Q8, bool ROLE0, class F>
 TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, signed char* xq, float* xsc,
                      const float* rmsw, float* red, float* sqa, int wave, int lane, unsigned long long* ts, F&& mid) {
   const int n4 = d.K >> 2, pad4 = Q8 ? n4 : g.nch * PL * 64;
-  if (Q8 && d.kind == PK_WO) {
-    // the attention units published the Wo input already quantised (attention.hpp
-    // publish_head): {4 codes, tag} granules, two per 16-byte load, and {scale, tag} granules
-    mid();
-    const auto rq = rsrc_of(p.gxq);
-    const bool hs = threadIdx.x < d.K / 64;  // (K / 64 <= PT for every supported dim)
-    unsigned long long s0 = 0;
-    if (hs) s0 = ld8_sc1(p.gxs + threadIdx.x);  // in flight with the code loads
-    for (int j = threadIdx.x; j < d.K / 8; j += PT) {
-      v4u a = ld16_sc1(rq, (unsigned)j * 16u);
-      for (unsigned spins = 0; a.y != d.tag_in || a.w != d.tag_in; ++spins) {
-        if ((spins & 255) == 255 &&
-            (spins > kGranSpinLimit || __hip_atomic_load(as_g32(p.err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-          __hip_atomic_store(as_g32(p.err), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        a = ld16_sc1(rq, (unsigned)j * 16u);
-      }
-      *reinterpret_cast<uint2*>(xq + j * 8) = make_uint2(a.x, a.z);
-    }
-    if (hs)
-      xsc[threadIdx.x] = (unsigned)(s0 >> 32) == d.tag_in ? __uint_as_float((unsigned)s0)
-                                                          : gran_wait(p.gxs + threadIdx.x, d.tag_in, p.err);
-    if (ts && lane == 0) ts[wave == 0 ? 8 : 10] = __builtin_amdgcn_s_memrealtime();  // input gathered
-    if (ts && lane == 0 && wave == 0) ts[9] = __builtin_amdgcn_s_memrealtime();
-    __syncthreads();
-    return;
-  }
-  if (Q8 && !d.rms && d.gin) {  // W2: quantised while it is gathered
+  if (Q8 && !d.rms && d.gin) {  // Wo, W2: quantised while it is gathered
     gather_q8<SB>(rsrc_of(d.gin), d.tag_in, n4, g.nch, xq, xsc, p.err, mid);
     if (ts && lane == 0) ts[wave == 0 ? 8 : 10] = __builtin_amdgcn_s_memrealtime();  // input gathered
     if (ts && lane == 0 && wave == 0) ts[9] = __builtin_amdgcn_s_memrealtime();
@@ -563,8 +528,8 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, sign
     float t;
     if constexpr (Q8) {
       __syncthreads();  // the squares are in sqa
-      if (wave == 0) {
-        const float v = wave_seqsum(sqa, d.K, lane);
+      if constexpr (ROLE0) {
+        const float v = d.K <= 4096 ? wave_seqsum_reg(sqa, d.K, lane) : wave_seqsum(sqa, d.K, lane);
         if (lane == 0) red[0] = v;
       }
       __syncthreads();
@@ -634,7 +599,7 @@ TL_DEVICE float2 rope_cs(const PStep& p, int row) {
 // xres: this block's slice of the residual stream x (rows i0.. of the dim-row phases, the
 // same slice for Wo and W2), kept in LDS so the residual add never re-reads x.
 TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const float* res, float* xres, int lane,
-                        int l, float2 cs0, const float* pbuf) {
+                        int l, float2 cs0, const float* pbuf, const uint64_t* etab) {
   unsigned long long best = 0;
   for (int it = lane; it < g.ni; it += 64) {
     float v[2] = {0.f, 0.f};
@@ -642,12 +607,7 @@ TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const flo
       float s;
       if (p.q8 && g.nch > 1) {
         // int8 rows longer than a chunk: runq's chain over the row's group products (runq.c:330-338)
-        const f4* pr = reinterpret_cast<const f4*>(pbuf + (it * d.rpi + r) * p.pgp);
-        s = 0.f;
-        for (int k = 0; k < (d.K >> 8); ++k) {
-          const f4 x = pr[k];
-          s = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(s, x.x), x.y), x.z), x.w);
-        }
+        s = chain_f4(reinterpret_cast<const f4*>(pbuf + (it * d.rpi + r) * p.pgp), d.K >> 8, 0.f);
       } else {
         const float* rr = res + (it * d.rpi + r) * g.nch;
         s = rr[0];
@@ -665,7 +625,7 @@ TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const flo
       st8_sc1(d.gout + item, gran(d.tag_out, xres[it]));
       if (d.kind == PK_DOWN && l == p.L - 1) p.x[item] = xres[it];  // final residual stream (state)
     } else if (d.kind == PK_UP) {
-      st8_sc1(d.gout + item, gran(d.tag_out, silu_mul(v[0], v[1])));
+      st8_sc1(d.gout + item, gran(d.tag_out, silu_mul_tab(v[0], v[1], etab)));
     } else {  // PK_QKV: RoPE (src/seq.cpp:86-101), q / k_new / v_new granules, KV-cache row
       const int row = 2 * item;
       const int pb = p.pos[0];
@@ -734,9 +694,9 @@ TL_DEVICE void grid_barrier(const PStep& p) {
 // The phase sequence as seen by one wave.  ROLE0 = the control wave (epilogues, attention,
 // norm preloads); the other waves stream.  Both execute the same workgroup barriers.
 template <int HS, bool ROLE0, bool Q8>
-TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* res, float* xres, float* red,
+TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xres, float* red,
                       float* rmsw, f4* xs, signed char* xq, float* xsc, float* sqa, float* scr, float* cwb,
-                      unsigned tb) {
+                      const uint64_t* etab, unsigned tb) {
   const int G = gridDim.x;
   const int nph = 5 * p.L + 1;
   unsigned* ctr = reinterpret_cast<unsigned*>(red + 15);  // dynamic slot counter (red[0..PW) is the norm sum)
@@ -763,23 +723,26 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
         aw.a.kv_mul = p.kv_mul; aw.a.seq_len = p.S; aw.a.nsplit = p.NS; aw.a.min_chunk = 16;
         aw.cnt = p.tickets + (long long)l * p.H; aw.B = 1; aw.NS = p.NS;
         aw.gqkv = p.gqkv; aw.gout = p.gxb;
-        if (Q8) { aw.gq8 = p.gxq; aw.gq8s = p.gxs; }  // the Wo input leaves quantised
+        aw.gsc = p.gsc; aw.etab = etab;
         aw.tag_in = tb + 5u * l + 1; aw.tag_out = tb + 5u * l + 2; aw.err = p.err;
         aw.ts = p.trace ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots + 8 : nullptr;
         if constexpr (Q8) {
-          // int8: runq's attention bit for bit, one unit per head (attention.hpp attn_unit_exact)
-          for (int u = blockIdx.x; u < p.H; u += G) attn_unit_exact<HS, true>(aw, 0, u, scr, lane);
+          // int8: runq's attention bit for bit, each head split over p.ang units (attention.hpp
+          // attn_unit_split).  K / V go through the fp32 staging strip xs: nothing reads it before
+          // the next normed staging (FFN-up), which this block starts after this unit.
+          for (int u = blockIdx.x; u < p.H * p.ang; u += G)
+            attn_unit_split<HS>(aw, u / p.ang, u % p.ang, p.ang, scr, reinterpret_cast<float*>(xs), p.pad_floats, lane);
         } else {
           const int units = p.H * p.NS;
-          for (int u = blockIdx.x; u < units; u += G) attn_unit<HS, 16, true>(aw, u, strips, lane);
+          for (int u = blockIdx.x; u < units; u += G) attn_unit<HS, 16, true>(aw, u, lane);
         }
         TRACE(3);
         continue;
       }
       const PDesc d = make_desc<Q8>(p, kind, l, tb);
       const PGeo g = geo<Q8>(d);
-      stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, sqa, wave, lane,
-                p.trace ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots : nullptr, [] {});
+      stage<Q8, true>(d, g, p, xs, xq, xsc, rmsw, red, sqa, wave, lane,
+                      p.trace ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots : nullptr, [] {});
       TRACE(1);
       float2 cs0 = make_float2(1.f, 0.f);
       if (kind == PK_QKV) {
@@ -790,7 +753,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
       __syncthreads();  // every slot reduced into res
       if (lane == 0) *ctr = 0u;  // next GEMV phase's slot counter (used after its staging barrier)
       TRACE(2);
-      epilogue(d, g, p, res, xres, lane, l, cs0, scr);
+      epilogue(d, g, p, res, xres, lane, l, cs0, scr, etab);
       TRACE(3);
     }
   } else {
@@ -823,8 +786,8 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* strips, float* 
 #pragma unroll
         for (int i = pfn<Q8>(); i < NBUF; ++i) load_any<Q8>(d, g, p, sw + i * NSW, lane, buf[i], sc[i]);
       };
-      stage<Q8>(d, g, p, xs, xq, xsc, rmsw, red, sqa, wave, lane,
-                tr ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots : nullptr, mid);
+      stage<Q8, false>(d, g, p, xs, xq, xsc, rmsw, red, sqa, wave, lane,
+                       tr ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots : nullptr, mid);
       if (tr) TRACE(4);
       run_gemv<Q8>(d, g, p, sw, lane, xs, xq, xsc, res, buf, sc, ctr,
                    tr ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots + 5 : nullptr,
@@ -875,8 +838,7 @@ template <int HS, bool Q8>
 __global__ void __launch_bounds__(PT) persistent_step_kernel(PStep p) {
   if (p.fault && blockIdx.x == 0) return;  // test hook: a missing block (every wait is bounded)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* strips = reinterpret_cast<float*>(smem);  // 64: attention score strip of wave 0
-  float* xres = strips + 64;                        // kPResidFloats: residual slice
+  float* xres = reinterpret_cast<float*>(smem);     // kPResidFloats: residual slice
   float* res = xres + kPResidFloats;                // kPResFloats: row-chunk sums
   float* red = res + kPResFloats;                   // 16: block reductions
   float* rmsw = red + 16;                           // dim: the next norm's weights
@@ -888,16 +850,21 @@ __global__ void __launch_bounds__(PT) persistent_step_kernel(PStep p) {
   float* sqa = xsc + p.q8_pad / 64;
   float* scr = sqa + p.n_sqa;
   float* cwb = scr + p.n_scr;
+  uint64_t* etab = reinterpret_cast<uint64_t*>(cwb + p.n_cw);  // the expf table (32 doubles' bits)
+  {
+    constexpr uint64_t tab[32] = TL_EXPF_TABLE;
+    if (threadIdx.x < 32) etab[threadIdx.x] = tab[threadIdx.x];  // (read after the first barrier)
+  }
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const unsigned tb = p.seq[0] << 12;  // tag base of this launch
-  if (wave == 0) phases<HS, true, Q8>(p, wave, lane, strips, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, tb);
-  else phases<HS, false, Q8>(p, wave, lane, strips, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, tb);
+  if (wave == 0) phases<HS, true, Q8>(p, wave, lane, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, etab, tb);
+  else phases<HS, false, Q8>(p, wave, lane, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, etab, tb);
 }
 
 static size_t lds_bytes(const PStep& p) {
-  return (size_t)(64 + kPResidFloats + kPResFloats + 16 + p.dim + p.pad_floats) * 4 + (size_t)p.q8_pad +
-         (size_t)p.q8_pad / 16 + (size_t)(p.n_sqa + p.n_scr + p.n_cw) * 4;
+  return (size_t)(kPResidFloats + kPResFloats + 16 + p.dim + p.pad_floats) * 4 + (size_t)p.q8_pad +
+         (size_t)p.q8_pad / 16 + (size_t)(p.n_sqa + p.n_scr + p.n_cw) * 4 + 32 * 8;
 }
 
 template <int HS, bool Q8>
@@ -931,6 +898,11 @@ bool persistent_prepare(PStep& p, int ncu, const char** why) {
     return (int)((long long)n_items * (100 + kXcdSkew) / part_weight(ncu) + 2) * rpi * nchunks(K);
   };
   p.pad_floats = padf(p.dim) > padf(p.hid) ? padf(p.dim) : padf(p.hid);
+  // int8: the exact attention splits each head over ang units (<= 8, at most one per block, >= 8
+  // columns each; attention.hpp attn_unit_split)
+  p.ang = 1;
+  if (p.q8)
+    while (p.ang < 8 && (long long)p.H * p.ang * 2 <= ncu && p.hs / (p.ang * 2) >= 8) p.ang *= 2;
   p.q8_pad = p.q8 ? 4096 * (nchunks(p.dim) > nchunks(p.hid) ? nchunks(p.dim) : nchunks(p.hid)) : 0;
   p.n_sqa = p.n_scr = p.n_cw = p.pgp = 0;
   if (p.q8) {
@@ -961,6 +933,16 @@ bool persistent_prepare(PStep& p, int ncu, const char** why) {
     return fail("too many rows per block");
   if ((long long)p.dim * (100 + kXcdSkew) / part_weight(ncu) + 2 > kPResidFloats)
     return fail("residual slice per block too large");
+  if (p.q8) {
+    // the strip xs doubles as the attention unit's LDS window: a round of 64 keys and then V rows
+    // of hs / ang floats, 512 rows a round (64 when the LDS is short)
+    const int base = p.pad_floats;
+    for (int rows : {512, 64}) {
+      const int need = 64 * p.hs + rows * (p.hs / p.ang);
+      p.pad_floats = base > need ? base : need;
+      if (lds_bytes(p) <= 160 * 1024) break;
+    }
+  }
   if (lds_bytes(p) > 160 * 1024) return fail("activations do not fit the LDS");
   {  // allow more than 64 KiB of dynamic LDS (gfx950: 160 KiB per CU): a per-device attribute,
      // raised once for each device a decoder is prepared on (decoders of several devices may be

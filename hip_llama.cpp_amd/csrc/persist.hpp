@@ -17,7 +17,7 @@ struct PStep {
   int* out;                 // [S] greedy tokens by position (argmax tail), may be null
   // hand-off granules {value, tag} (zero once at allocation; tags are never 0)
   unsigned long long *gx, *gxb, *ghb, *gqkv;  // [dim], [dim], [hidden], [dim + 2*kv_dim]
-  unsigned long long *gxq, *gxs;  // int8: the attention output quantised, {4 codes, tag} [dim/4], {scale, tag} [dim/64]
+  unsigned long long* gsc;   // int8: attention score granules [H][S] (attention.hpp attn_unit_split)
   unsigned* sync;           // kPSyncWords barrier shards, zeroed before every launch
   unsigned* err;            // sticky: a wait gave up (1: barrier, 2: hand-off)
   unsigned* seq;            // launch sequence (tags), advanced by the kernel
@@ -40,6 +40,7 @@ struct PStep {
   int n_sqa, n_scr, n_cw;   // Q8 (exact arithmetic) LDS floats: norm squares, long-row products /
                             // attention strip, streaming-wave chain scratch (persistent_prepare)
   int pgp;                  // Q8: row stride (floats) of the long-row products
+  int ang;                  // Q8: attention units per head (persistent_prepare)
   int fault;                // test hook (THALLAMA_OPT_PERSIST_FAULT): block 0 exits at once, as
                             // if the grid were not co-resident; every other wait gives up
 };

@@ -52,6 +52,25 @@ TL_DEVICE double lane_d(double v, int l) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+// s = fl(s + x) over the n4 float4s at p (LDS), in order, reading 8 float4 per batch (the
+// compiler waits for all of a batch's LDS reads at the first use: one latency per 32 elements).
+TL_DEVICE float chain_f4(const f4* p, int n4, float s) {
+  for (int j0 = 0; j0 < n4; j0 += 8) {
+    f4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = j0 + k < n4 ? p[j0 + k] : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (j0 + k < n4) {
+        s = __fadd_rn(s, v[k].x);
+        s = __fadd_rn(s, v[k].y);
+        s = __fadd_rn(s, v[k].z);
+        s = __fadd_rn(s, v[k].w);
+      }
+  }
+  return s;
+}
+
 // s = fl(s + x) over the ch4 float4s of one chunk, in order.
 TL_DEVICE float chunk_chain(const float* my, int ch4, float s) {
   const f4* p = reinterpret_cast<const f4*>(my);
@@ -104,6 +123,87 @@ TL_DEVICE float wave_seqsum(const float* a, int n, int lane) {
     lo = c + 1;
   }
   return lane_f(e, 63);  // not reached: every round proves at least one more lane
+}
+
+// The same sum with each lane's chunk held in registers (ch <= 64, i.e. n <= 4096): the rounds'
+// re-chains are register-only (an LDS read per element put ~100 cycles of latency on every
+// step of every round).  Identical result.
+TL_DEVICE float reg_chain(const f4 (&r)[16], int ch4, float s) {
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    if (k < ch4) {
+      s = __fadd_rn(s, r[k].x);
+      s = __fadd_rn(s, r[k].y);
+      s = __fadd_rn(s, r[k].z);
+      s = __fadd_rn(s, r[k].w);
+    }
+  return s;
+}
+
+TL_DEVICE float wave_seqsum_reg(const float* a, int n, int lane) {
+  const int ch = seqsum_ch(n), ch4 = ch >> 2;
+  const f4* my = reinterpret_cast<const f4*>(a + lane * (ch + 4));
+  f4 r[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) r[k] = k < ch4 ? my[k] : f4{0.f, 0.f, 0.f, 0.f};
+  float e = reg_chain(r, ch4, 0.f);
+  double inc = (double)e;
+  float start = lane == 0 ? 0.f : (float)(wave_incl_scan_d(inc) - inc);
+  e = reg_chain(r, ch4, start);
+  inc = (double)e - (double)start;
+  // one prefix of the guessed increments serves every round: a round re-bases the lanes above
+  // the last proven one on its value (P[L] - P[lo] = the increments in between); a lane whose
+  // increment depends on its start (a binade crossing, a tie) fails in its round and is fixed
+  const double incl = wave_incl_scan_d(inc);
+  const double pre = incl - inc;  // exclusive
+  const float total0 = (float)lane_d(incl, 63);
+  int lo = 0;
+  float slo = 0.f;     // proven start of lane lo
+  double plo = 0.0;    // pre[lo]
+  for (int round = 0; round < 64; ++round) {
+    if (lane > lo) start = (float)((double)slo + (pre - plo));
+    const float total = round == 0 ? total0 : (float)((double)slo + (lane_d(incl, 63) - plo));
+    e = reg_chain(r, ch4, start);
+    float next = __shfl_down(start, 1, 64);
+    if (lane == 63) next = total;
+    const unsigned long long bad = __ballot(lane >= lo && __float_as_uint(e) != __float_as_uint(next) &&
+                                            !(e != e && next != next));
+    if (!bad) return total;
+    const int c = (int)__builtin_ctzll(bad);
+    const float ec = lane_f(e, c);
+    if (c == 63) return ec;
+    lo = c + 1;
+    slo = ec;
+    plo = lane_d(pre, lo);
+    if (lane == lo) start = ec;
+  }
+  return lane_f(e, 63);
+}
+
+// Short sums (n <= 512): the chain itself, run by every lane over the values read back from the
+// seqsum layout (broadcast LDS reads, a float4 at a time).  The layout's padding must be zero
+// (s + 0 = s for the chain's s >= +0, so whole float4s are added).  Reads in batches of 12
+// float4 (the compiler waits for all of a batch's LDS reads at the first use).
+TL_DEVICE float wave_seqsum_short(const float* a, int n) {
+  const int ch4 = seqsum_ch(n) >> 2, n4 = (n + 3) >> 2;  // ch4 = 1 or 2
+  const f4* a4 = reinterpret_cast<const f4*>(a);
+  float s = 0.f;
+  for (int j0 = 0; j0 < n4; j0 += 12) {
+    f4 v[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {  // float4 j of the sequence: rows of ch4 + 1 float4s
+      const int j = j0 + k;
+      v[k] = j < n4 ? a4[ch4 == 1 ? 2 * j : j + (j >> 1)] : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+      s = __fadd_rn(s, v[k].x);
+      s = __fadd_rn(s, v[k].y);
+      s = __fadd_rn(s, v[k].z);
+      s = __fadd_rn(s, v[k].w);
+    }
+  }
+  return s;
 }
 
 }  // namespace tl

@@ -177,6 +177,7 @@ def lib():
             "thallama_memset": (I, [VP, I, S]),
             "thallama_sync": (I, []),
             "thallama_seqsum_check": (I, [VP, I, I, VP]),
+            "thallama_seqsum_time": (I, [VP, I, I, VP, VP]),
             "thallama_last_error": (C.c_char_p, []),
         }
         for name, (res, args) in sig.items():

@@ -124,6 +124,8 @@ int thallama_gemv_bench(int mode, int M, int K, int nb, int ipw, int waves, int 
 /* Test hook: the wave-parallel left-to-right fp32 sum (csrc/seqsum.hpp) of `count` arrays of n
  * floats (device in_d, n <= 8192) into out_d[count]; synchronous. */
 int thallama_seqsum_check(const float* in_d, int n, int count, float* out_d);
+/* Same with the register form (n <= 4096), plus the clock cycles of each call in cyc_d[count]. */
+int thallama_seqsum_time(const float* in_d, int n, int count, float* out_d, long long* cyc_d);
 
 /* ---- synthetic weights ------------------------------------------------- */
 /* Fill a v0 arena (layout of thallama_map_weights) with the deterministic synthetic

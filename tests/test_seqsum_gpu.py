@@ -50,3 +50,22 @@ def test_wave_seqsum_bitexact(gpu, kind, n):
     got = dout.download(np.float32)
     want = np.array([seq_chain(r) for r in a], np.float32)
     np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("kind", ["gauss_sq", "ints_sq", "softmax"])
+@pytest.mark.parametrize("n", [4096, 768, 200])
+def test_wave_seqsum_reg_bitexact(gpu, kind, n):
+    """The register form (n <= 4096; the norm and softmax sums of the int8 step) is the chain too;
+    it also reports clock cycles per call (printed)."""
+    rng = np.random.default_rng(n * 11 + len(kind))
+    count = 64
+    a = np.ascontiguousarray(arrays(kind, n, count, rng), np.float32)
+    din = gpu.DevBuf.from_array(a)
+    dout = gpu.DevBuf(4 * count)
+    dcyc = gpu.DevBuf(8 * count)
+    gpu.check(gpu.lib().thallama_seqsum_time(din.ptr, n, count, dout.ptr, dcyc.ptr), "seqsum_time")
+    got = dout.download(np.float32)
+    want = np.array([seq_chain(r) for r in a], np.float32)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+    cyc = dcyc.download(np.int64)
+    print(f"seqsum_reg {kind} n={n}: cycles median {int(np.median(cyc))} max {int(cyc.max())}")

@@ -106,14 +106,15 @@ def main():
         print(f"{kind:9s}" + "".join(f"{v:8.2f}" for v in row))
         out[kind + "_staging"] = row
     # attention phase on the blocks that run a unit (single-chunk contexts): q granule ready,
-    # k/v granules ready, output computed, unit done (us after the phase start)
+    # (int8: every score of the head gathered; fp32: k/v granules ready), output computed, unit
+    # done (us after the phase start)
     att = [ph for ph in range(1, nph - 1, 5)]
     a = np.stack([t[:, ph, :] for ph in att])  # [layers][G][slots]
     live = a[:, :, 10] > a[:, :, 0]
     if live.any():
         rel = lambda k: float(np.median((a[:, :, k] - a[:, :, 0])[live]))
-        print(f"attention units ({int(live.sum() / len(att))} per layer): q {rel(8):.2f}  kv {rel(9):.2f}  "
-              f"computed {rel(10):.2f}  done {rel(3):.2f} us after phase start")
+        print(f"attention units ({int(live.sum() / len(att))} per layer): q {rel(8):.2f}  scores/kv {rel(9):.2f}  "
+              f"summed {rel(11):.2f}  computed {rel(10):.2f}  done {rel(3):.2f} us after phase start")
     # epilogue (all slots reduced -> epilogue issued), median and max over blocks
     print("epilogue us (median / max over blocks): " + "  ".join(
         f"{kind} {np.median([np.median(t[:, ph, 3] - t[:, ph, 2]) for ph in range(k, nph - 1, 5)]):.2f}/"

@@ -52,6 +52,40 @@ static float wave_seqsum(const float* a, int n, int* rounds) {
   }
 }
 
+/* the variant with one prefix of the guessed increments for every round (csrc/seqsum.hpp
+ * wave_seqsum_reg) */
+static float wave_seqsum_1p(const float* a, int n, int* rounds) {
+  const int CH = (n + 63) / 64;
+  float pad[64 * 256];
+  memset(pad, 0, sizeof(float) * 64 * CH);
+  memcpy(pad, a, sizeof(float) * n);
+  double part[64], pre[65], inc[64];
+  float start[64], e[64];
+  for (int L = 0; L < 64; ++L) part[L] = chain(pad + L * CH, CH, 0.f);
+  pre[0] = 0; for (int L = 0; L < 64; ++L) pre[L + 1] = pre[L] + part[L];
+  for (int L = 0; L < 64; ++L) {
+    start[L] = L ? (float)pre[L] : 0.f;
+    inc[L] = (double)chain(pad + L * CH, CH, start[L]) - (double)start[L];
+  }
+  pre[0] = 0; for (int L = 0; L < 64; ++L) pre[L + 1] = pre[L] + inc[L];
+  int lo = 0; float slo = 0.f; double plo = 0.0;
+  *rounds = 0;
+  for (;;) {
+    for (int L = lo + 1; L < 64; ++L) start[L] = (float)((double)slo + (pre[L] - plo));
+    const float total = (float)((double)slo + (pre[64] - plo));
+    int bad = -1;
+    for (int L = lo; L < 64; ++L) {
+      e[L] = chain(pad + L * CH, CH, start[L]);
+      const float next = L + 1 < 64 ? start[L + 1] : total;
+      if (bad < 0 && e[L] != next) bad = L;
+    }
+    ++*rounds;
+    if (bad < 0) return total;
+    if (bad == 63) return e[63];
+    lo = bad + 1; slo = e[bad]; plo = pre[lo]; start[lo] = slo;
+  }
+}
+
 static unsigned long long rs = 88172645463325252ull;
 static double urand(void) { rs ^= rs << 13; rs ^= rs >> 7; rs ^= rs << 17; return (rs >> 11) * (1.0 / 9007199254740992.0); }
 static double nrand(void) { double u = urand() + 1e-300, v = urand(); return sqrt(-2 * log(u)) * cos(6.283185307179586 * v); }
@@ -76,9 +110,11 @@ int main(void) {
         float xf = (float)x;
         a[i] = xf * xf;
       }
-      int r;
-      float got = wave_seqsum(a, n, &r), want = chain(a, n, 0.f);
+      int r, r1;
+      float got = wave_seqsum(a, n, &r), want = chain(a, n, 0.f), got1 = wave_seqsum_1p(a, n, &r1);
       if (memcmp(&got, &want, 4)) ++bad;
+      if (memcmp(&got1, &want, 4)) ++bad;
+      if (r1 > r) r = r1;
       hist[r < 69 ? r : 69]++;
       if (r > worst) worst = r;
     }
