@@ -589,11 +589,12 @@ TL_DEVICE void attn_unit_split(const AttnWaveParams& w, int h, int c, int NG, fl
   if (w.ts && lane == 0) w.ts[1] = __builtin_amdgcn_s_memrealtime();
   mx = wave_max_u(mx);  // exact (a maximum)
   wave_lds_fence();
-  for (int t = lane; t < T; t += 64) sa[seqsum_index(t, ch)] = expf_libm_tab(__fsub_rn(at[t], mx), w.etab);
+  const unsigned chm = seqsum_magic(ch);
+  for (int t = lane; t < T; t += 64) sa[seqsum_index_m(t, ch, chm)] = expf_libm_tab(__fsub_rn(at[t], mx), w.etab);
   wave_lds_fence();
   const float sum = T <= 512 ? wave_seqsum_short(sa, T) : T <= 4096 ? wave_seqsum_reg(sa, T, lane) : wave_seqsum(sa, T, lane);
   if (w.ts && lane == 0) w.ts[3] = __builtin_amdgcn_s_memrealtime();
-  for (int t = lane; t < T; t += 64) at[t] = __fdiv_rn(sa[seqsum_index(t, ch)], sum);
+  for (int t = lane; t < T; t += 64) at[t] = __fdiv_rn(sa[seqsum_index_m(t, ch, chm)], sum);
   wave_lds_fence();
   // this unit's columns: lane < CW owns column col0 + lane, a chain over t
   float o = 0.f;

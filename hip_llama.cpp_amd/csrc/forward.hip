@@ -124,6 +124,8 @@ struct thallama_decoder {
   int* pos_h = nullptr;
   float2* rope_d = nullptr;
   float* xn_d = nullptr;        // [<=16][dim] normed rows for the matrix-core GEMV (batch >= 2)
+  float* ssq_d = nullptr;       // [B][dim/16] per-tile sums of squares carried from Wo / W2 to the next norm
+  bool no_ssq = false;          // THALLAMA_NO_SSQ=1: the norm prologue launch instead (A/B measurement)
   signed char* xq_d = nullptr;  // int8 batched: activations quantised once per launch [8][max(dim, hidden)]
   float* xqs_d = nullptr;       //   and their group scales
   signed char* hq_d = nullptr;  // int8 4..8 sequences: SwiGLU output quantised for W2 [8][hidden]
@@ -212,6 +214,11 @@ static int auto_splits(const thallama_decoder* d) {
   return ns;
 }
 
+// Hand-off granules of the persistent step: x | xb | hb | q k v | int8 attention scores [H][S].
+static size_t granule_count(const thallama_decoder* d) {
+  return (size_t)3 * d->dim + d->hidden + 2 * d->kv_dim + (size_t)d->H * d->S + 2;
+}
+
 extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg, const TransformerWeights* w,
                                        const RunState* s, int batch, hipStream_t stream) {
   if (!out || !cfg || !w || !s || batch <= 0) {
@@ -267,6 +274,9 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
   if (batch >= 2) {
     const size_t nblk = (size_t)tl::mfma_target_blocks();
     TL_TRY(hipMalloc(&d->xn_d, sizeof(float) * (size_t)(batch < 16 ? batch : 16) * d->dim));
+    TL_TRY(hipMalloc(&d->ssq_d, sizeof(float) * (size_t)batch * ((d->dim + 15) / 16)));
+    const char* e = getenv("THALLAMA_NO_SSQ");
+    d->no_ssq = e && e[0] == '1';
     TL_TRY(hipMalloc(&d->mpart_d, sizeof(float) * nblk * 2 * 256));
     TL_TRY(hipMalloc(&d->mcnt_d, sizeof(unsigned) * nblk));
     TL_TRY(hipMemset(d->mcnt_d, 0, sizeof(unsigned) * nblk));
@@ -299,8 +309,7 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
     TL_TRY(hipMalloc(&d->psync, sizeof(unsigned) * (d->psync_zero + 32)));
     TL_TRY(hipMemset(d->psync, 0, sizeof(unsigned) * (d->psync_zero + 32)));
     TL_TRY(hipMalloc(&d->pbmax, sizeof(unsigned long long) * d->ncu));
-    // x | xb | hb | qkv | int8 attention scores [H][S]
-    const size_t ng = (size_t)3 * d->dim + d->hidden + 2 * d->kv_dim + (size_t)d->H * d->S + 2;
+    const size_t ng = granule_count(d);
     TL_TRY(hipMalloc(&d->pgran, sizeof(unsigned long long) * ng));
     TL_TRY(hipMemset(d->pgran, 0, sizeof(unsigned long long) * ng));
   }
@@ -320,6 +329,7 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   (void)hipHostFree(d->pos_h);
   (void)hipFree(d->rope_d);
   (void)hipFree(d->xn_d);
+  (void)hipFree(d->ssq_d);
   (void)hipFree(d->mpart_d);
   (void)hipFree(d->xq_d);
   (void)hipFree(d->xqs_d);
@@ -408,6 +418,20 @@ static int q8_ffn_quant(const thallama_decoder* d) {
 }
 
 // Enqueue one decode step reading tok_d / pos_d; logits land in s.logits.
+// fp32 batched steps on the matrix cores: the residual launches (Wo, W2) leave per-tile sums of
+// squares of the residual stream and the next normed launch reduces them instead of running a
+// norm prologue launch (gemv_mfma.hpp).  Both ends use the matrix-core kernel or neither (same nb).
+static void ssq_to_next_norm(const thallama_decoder* d, tl::GemvParams& p) {
+  if (d->q8 || !d->ssq_d) return;
+  p.ssq_out = d->ssq_d;
+  p.ssq_nt = (d->dim + 15) / 16;
+}
+static void norm_from_ssq(const thallama_decoder* d, tl::GemvParams& p) {
+  if (d->q8 || !d->ssq_d || d->no_ssq || (d->dim + 15) / 16 > 256) return;  // (the kernel sums <= 256 tiles)
+  p.ssq_in = d->ssq_d;
+  p.ssq_nt = (d->dim + 15) / 16;
+}
+
 static int enqueue_step(thallama_decoder* d) {
   const int dim = d->dim, hid = d->hidden, kvd = d->kv_dim, S = d->S;
   const long long kv_b_stride = (long long)d->L * S * kvd;
@@ -428,6 +452,7 @@ static int enqueue_step(thallama_decoder* d) {
       p.x_stride = dim;
       p.rms_w = w.rms_att_weight + ll * dim;
       p.xn = d->xn_d;
+      if (l > 0) norm_from_ssq(d, p);
       if (l == 0) {
         p.tok = d->tok_d;
         p.emb = w.token_embedding_table;
@@ -524,6 +549,7 @@ static int enqueue_step(thallama_decoder* d) {
       p.y = s.x;
       p.y_stride = dim;
       p.xq_ready = q8_attn_quant(d);
+      ssq_to_next_norm(d, p);
       int ev = prof_begin(d);
       TL_TRY(gemv(d, tl::GM_RESID, p, Q8L(wo), nullptr, nullptr));
       prof_end(d, THALLAMA_K_WO, ev);
@@ -540,6 +566,7 @@ static int enqueue_step(thallama_decoder* d) {
       p.x_stride = dim;
       p.rms_w = w.rms_ffn_weight + ll * dim;
       p.xn = d->xn_d;
+      norm_from_ssq(d, p);
       p.y = s.hb;
       p.y_stride = hid;
       if (d->hq_d) {
@@ -567,6 +594,7 @@ static int enqueue_step(thallama_decoder* d) {
         p.xqs = d->hqs_d;
         p.xq_ready = 1;
       }
+      ssq_to_next_norm(d, p);
       int ev = prof_begin(d);
       TL_TRY(gemv(d, tl::GM_RESID, p, Q8L(w2), nullptr, nullptr));
       prof_end(d, THALLAMA_K_FFN_DOWN, ev);
@@ -583,6 +611,7 @@ static int enqueue_step(thallama_decoder* d) {
     p.x_stride = dim;
     p.rms_w = w.rms_final_weight;
     p.xn = d->xn_d;
+    if (d->L > 0) norm_from_ssq(d, p);
     if (d->L == 0) {
       p.tok = d->tok_d;
       p.emb = w.token_embedding_table;
@@ -669,10 +698,10 @@ extern "C" int thallama_decoder_persistent(thallama_decoder* d) { return d && us
 extern "C" int thallama_persistent_cooperative(void) { return tl::persistent_cooperative() ? 1 : 0; }
 
 // Diagnostics: copy the persistent step's hand-off granules {value, tag} (x | xb | hb | q k v |
-// int8 codes | scales, the last layer's values after a launch) to host (n granules at most).
+// int8 attention scores, the last layer's values after a launch) to host (n granules at most).
 extern "C" int thallama_decoder_granules(thallama_decoder* d, unsigned long long* host, size_t n) {
   if (!d || !d->pgran) return (int)hipErrorInvalidValue;
-  const size_t ng = (size_t)3 * d->dim + d->hidden + 2 * d->kv_dim + d->dim / 4 + d->dim / 64 + 2;
+  const size_t ng = granule_count(d);
   if (!host) return (int)ng;
   TL_TRY(hipStreamSynchronize(d->stream));
   TL_TRY(hipMemcpy(host, d->pgran, (n < ng ? n : ng) * 8, hipMemcpyDeviceToHost));

@@ -84,6 +84,13 @@ struct GemvParams {
   float* mpart;
   unsigned* mcnt;
   int msplit, msteps;    // set by the launcher: K splits per tile, 16-k steps per split
+  // matrix-core path, RMSNorm carried across launches (gemv_mfma.hpp): a RESID launch (Wo / W2)
+  // leaves per-tile partial sums of squares of the rows it updated in ssq_out[b * ssq_nt + tile];
+  // the next normed launch (ssq_in) reduces them in a fixed order and applies the norm as it
+  // loads its activations, instead of a gemv_prenorm_kernel launch
+  float* ssq_out;
+  const float* ssq_in;
+  int ssq_nt;            // tiles of the producing launch (its rows / 16)
 };
 
 // Blocks the matrix-core GEMV aims for: kMfmaDepth per CU (env THALLAMA_MFMA_DEPTH).

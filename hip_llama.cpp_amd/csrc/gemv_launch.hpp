@@ -93,15 +93,19 @@ inline hipError_t launch_mode(const GemvParams& p0, hipStream_t s, const GemvCfg
       if (MODE == GM_STORE) p.y_off += (long long)b0 * p.y_stride;
       else p.y += (long long)b0 * p.y_stride;
       if (p.kc) p.kc += (long long)b0 * p.kv_b_stride;
+      if (p.ssq_out) p.ssq_out += (long long)b0 * p.ssq_nt;
+      if (p.ssq_in) p.ssq_in += (long long)b0 * p.ssq_nt;
       if (p.vc) p.vc += (long long)b0 * p.kv_b_stride;
     }
     const GemvCfg c = cfg ? *cfg : gemv_default_cfg(MODE, p.n_items, p.K, p.nb, nt);
     hipError_t e;
     if (!cfg && p.nb >= gemv_mfma_min_nb() && (p.K & 15) == 0 && (p.x_stride & 3) == 0 &&
-        ((!p.rms_w && !p.tok) || p.xn)) {
-      // several sequences: the matrix-core kernel (gemv_mfma.hpp); a norm / embedding
-      // prologue runs once into the scratch rows first
-      if (p.rms_w || p.tok) {
+        ((!p.rms_w && !p.tok) || p.xn || (p.rms_w && p.ssq_in && !p.tok))) {
+      // several sequences: the matrix-core kernel (gemv_mfma.hpp); an embedding prologue, or a
+      // norm whose sums of squares the previous launch did not leave (ssq_in), runs once into
+      // the scratch rows first; otherwise the kernel applies the norm itself
+      if (p.tok || (p.rms_w && !p.ssq_in)) {
+        p.ssq_in = nullptr;
         hipLaunchKernelGGL(gemv_prenorm_kernel, dim3(p.nb), dim3(256), 0, s, p);
         p.x = p.xn;
         p.x_stride = p.K;

@@ -16,6 +16,11 @@
 // launch (gemv_prenorm_kernel, x' = w * (ss * x) as in src/seq.cpp:3-16) into scratch
 // rows, not once per block.  The fp32 MFMA accumulates exactly-rounded products in fp32,
 // within the reference's 1e-4 logits tolerance of its sequential loop.
+// RMSNorm across launches: the residual launches (Wo, W2) also leave, per 16-row tile, the sum of
+// squares of the rows they updated (a fixed order: rows 0..15 of the tile); the next normed
+// launch (QKV, W1/W3, classifier) reduces those partials in a fixed order at its start (every
+// block gets the same ss) and applies x' = w * (ss * x) as it loads the activations, so the
+// prologue launch runs only where the input is the embedding row (layer 0).
 #pragma once
 #include "gemv.hpp"
 
@@ -119,8 +124,11 @@ __global__ void __launch_bounds__(kMfmaWaves * 64) gemv_mfma_kernel(GemvParams p
   static_assert(XI >= 1 && XI <= NI, "live activation load instructions");
   constexpr int STR = U * 16 + 4;      // LDS row stride in floats (padded)
   constexpr int TILE = 16 * STR;       // floats per tile
+  static_assert(W * 64 == 256, "the norm and epilogue maps assume 256 threads");
   __shared__ __attribute__((aligned(16))) float lds[W * (NR + 1) * TILE];
   __shared__ unsigned s_last;
+  __shared__ float s_red[256];
+  __shared__ float s_ss[16];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int i = lane & 15, q = lane >> 4;
@@ -150,6 +158,33 @@ __global__ void __launch_bounds__(kMfmaWaves * 64) gemv_mfma_kernel(GemvParams p
     xrow[v] = p.x + (long long)(r < nb ? r : 0) * p.x_stride;
   }
 
+  // fused RMSNorm (p.rms_w set here only with p.ssq_in, see the launcher): ss_b from the producer's
+  // per-tile sums of squares (<= 256 tiles) — thread (b, j) sums tiles j, j + 16, ..., then b sums
+  // its 16 in order; run after the first weight loads are in flight (their latency covers it)
+  const bool fnorm = p.rms_w != nullptr;
+  float xs[NI];
+  auto norm_scales = [&] {
+    const int t = threadIdx.x, b = t >> 4, j = t & 15;
+    float part[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) part[k] = b < nb && j + 16 * k < p.ssq_nt ? p.ssq_in[(long long)b * p.ssq_nt + j + 16 * k] : 0.f;
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a = __fadd_rn(a, part[k]);
+    s_red[t] = a;
+    __syncthreads();
+    if (t < nb) {
+      float v = 0.f;
+      for (int k = 0; k < 16; ++k) v = __fadd_rn(v, s_red[t * 16 + k]);
+      s_ss[t] = __fdiv_rn(1.0f, sqrtf(__fadd_rn(__fdiv_rn(v, (float)K), 1e-5f)));  // src/seq.cpp:3-16
+    }
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < NI; ++v) {
+      const int r = RPI * v + lr;
+      xs[v] = r < nb ? s_ss[r] : 0.f;
+    }
+  };
   const int nsteps = K >> 4;
   const int s0 = split * p.msteps;
   const int s1 = s0 + p.msteps < nsteps ? s0 + p.msteps : nsteps;
@@ -172,9 +207,10 @@ __global__ void __launch_bounds__(kMfmaWaves * 64) gemv_mfma_kernel(GemvParams p
   // are issued (XI * RPI >= nb, a compile-time count: a run-time skip made the compiler's
   // vmcnt waits conservative), the other tile rows stay zero from the start
   auto xlive = [&](int v) { return v < XI; };
-  auto load = [&](f4 (&t)[NR + 1][NI], int g) {
+  auto load = [&](f4 (&t)[NR + 1][NI], f4& rw, int g) {
     bool ok;
     const int k = kof(g, ok);
+    if (fnorm) rw = *reinterpret_cast<const f4*>(p.rms_w + k);
 #pragma unroll
     for (int v = 0; v < NI; ++v) {
 #pragma unroll
@@ -192,12 +228,20 @@ __global__ void __launch_bounds__(kMfmaWaves * 64) gemv_mfma_kernel(GemvParams p
   f32x4 acc[NR];
 #pragma unroll
   for (int m = 0; m < NR; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mma = [&](const f4 (&t)[NR + 1][NI]) {
+  auto mma = [&](const f4 (&t)[NR + 1][NI], const f4& rw) {
 #pragma unroll
     for (int m = 0; m <= NR; ++m)
 #pragma unroll
       for (int v = 0; v < NI; ++v)
-        if (m < NR || xlive(v)) *reinterpret_cast<f4*>(my + m * TILE + (RPI * v + lr) * STR + 4 * lc) = t[m][v];
+        if (m < NR || xlive(v)) {
+          f4 e = t[m][v];
+          if (m == NR && fnorm) {  // x' = w * (ss * x), as gemv_prenorm_kernel (zeros stay zero)
+            const float sv = xs[v];
+            e = f4{__fmul_rn(rw.x, __fmul_rn(sv, e.x)), __fmul_rn(rw.y, __fmul_rn(sv, e.y)),
+                   __fmul_rn(rw.z, __fmul_rn(sv, e.z)), __fmul_rn(rw.w, __fmul_rn(sv, e.w))};
+          }
+          *reinterpret_cast<f4*>(my + m * TILE + (RPI * v + lr) * STR + 4 * lc) = e;
+        }
     asm volatile("" ::: "memory");  // same-wave LDS ops execute in order
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -215,13 +259,15 @@ __global__ void __launch_bounds__(kMfmaWaves * 64) gemv_mfma_kernel(GemvParams p
   };
 
   f4 ta[NR + 1][NI], tb[NR + 1][NI];
-  if (ng > 0) load(ta, 0);
+  f4 rwa = f4{0.f, 0.f, 0.f, 0.f}, rwb = rwa;
+  if (ng > 0) load(ta, rwa, 0);
+  if (fnorm) norm_scales();  // (block barriers: every wave, live or not)
   for (int g = 0; g < ng; g += 2) {
-    if (g + 1 < ng) load(tb, g + 1);
-    mma(ta);
+    if (g + 1 < ng) load(tb, rwb, g + 1);
+    mma(ta, rwa);
     if (g + 1 >= ng) break;
-    if (g + 2 < ng) load(ta, g + 2);
-    mma(tb);
+    if (g + 2 < ng) load(ta, rwa, g + 2);
+    mma(tb, rwb);
   }
 
   __syncthreads();  // the staging tiles become the wave-partial buffer
@@ -266,8 +312,25 @@ __global__ void __launch_bounds__(kMfmaWaves * 64) gemv_mfma_kernel(GemvParams p
         epi_one<MODE>(p, R, j, tot(0, t), tot(NR - 1, t));
       } else if constexpr (MODE == GM_QKV) {
         if ((row & 1) == 0) epi_one<MODE>(p, R >> 1, j, tot(0, t), tot(0, t + 16));
+      } else if constexpr (MODE == GM_RESID) {
+        float* y = p.y + (long long)j * p.y_stride + R;
+        const float nv = __fadd_rn(*y, tot(0, t));
+        *y = nv;
+        if (p.ssq_out) s_red[t] = __fmul_rn(nv, nv);
       } else {
         epi_one<MODE>(p, R, j, tot(0, t), 0.f);
+      }
+    }
+  }
+  if constexpr (MODE == GM_RESID) {
+    if (p.ssq_out) {  // this tile's sum of squares per sequence, rows in order (rows past the end: 0)
+      const int row = threadIdx.x >> 4, j = threadIdx.x & 15;
+      if (!(j < nb && tile * 16 + row < n_rows)) s_red[threadIdx.x] = 0.f;
+      __syncthreads();
+      if (threadIdx.x < nb) {
+        float v = 0.f;
+        for (int r = 0; r < 16; ++r) v = __fadd_rn(v, s_red[r * 16 + threadIdx.x]);
+        p.ssq_out[(long long)threadIdx.x * p.ssq_nt + tile] = v;
       }
     }
   }

@@ -89,6 +89,12 @@ TL_DEVICE float chunk_chain(const float* my, int ch4, float s) {
 // 64 lanes spread over the banks), zeros from n up to 64 ch.
 TL_DEVICE int seqsum_ch(int n) { return 4 * ((n + 255) >> 8); }
 TL_DEVICE int seqsum_index(int e, int ch) { return e / ch * (ch + 4) + e % ch; }
+// The same with the division by ch as a multiply-high (m = seqsum_magic(ch); exact for e < 2^20).
+TL_DEVICE unsigned seqsum_magic(int ch) { return 0xFFFFFFFFu / (unsigned)ch + 1u; }
+TL_DEVICE int seqsum_index_m(int e, int ch, unsigned m) {
+  const int q = (int)__umulhi((unsigned)e, m);
+  return e + 4 * q;  // q (ch + 4) + (e - q ch)
+}
 TL_DEVICE int seqsum_floats(int n) { return 64 * (seqsum_ch(n) + 4); }
 
 // The left-to-right fp32 sum of the n values laid out by seqsum_index in `a` (LDS).  One full

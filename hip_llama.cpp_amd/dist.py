@@ -44,3 +44,48 @@ def sum_over_ranks(value, device=None):
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def serve_sharded(requests_path, out_path, tokenizer_path, vocab_size, batch, step, max_token_len, max_seq_len,
+                  temperature=None, topp=0.9, prefill=None, workdir="."):
+    """The reference's test mode (test_data_parallelism, src/llama.cpp:891-1083) with one process
+    per GPU instead of one thread per GPU: every rank parses the request file
+    (read_inputfile, src/llama.cpp:424-453), serves the contiguous shard :func:`shard` gives it
+    through the host scheduler (``host.Requests.serve``: ``batch`` slots refilled from the shard,
+    one sampler per request) with its own ``step`` / ``prefill`` callbacks, and rank 0 gathers
+    the generated strings in request order and writes the output file (write_outputfile,
+    src/llama.cpp:455-505).  Every request is sampled independently (seed 314028 each), so the
+    file equals the single-process one byte for byte.  Returns the reference's num_gen_tokens
+    summed over ranks.  The only collectives are the object gather and that sum."""
+    import os
+
+    from . import host as H
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    full = H.Requests(requests_path, max_token_len, max_seq_len)
+    n = len(full)
+    a, b = shard(n, world, rank)
+    mine = [full.prompt(i) for i in range(a, b)]
+    del full
+    outs, gen = [], 0
+    if mine:
+        part = os.path.join(workdir, f".shard_{os.getpid()}_{rank}.txt")
+        with open(part, "wb") as f:
+            f.write(f"{len(mine)}\n".encode() + b"".join(p + b"\n" for p in mine))
+        try:
+            r = H.Requests(part, max_token_len, max_seq_len)
+        finally:
+            os.remove(part)
+        if temperature is not None:
+            r.set_sampling(temperature, topp)
+        gen = r.serve(tokenizer_path, vocab_size, 1, batch, step, prefill)
+        outs = [r.output(i) for i in range(len(mine))]
+    if world > 1:
+        parts = [None] * world
+        dist.all_gather_object(parts, outs)
+        outs = [o for p in parts for o in p]
+        gen = int(sum_over_ranks(gen))
+    if rank == 0:
+        with open(out_path, "wb") as f:
+            f.write(f"{n}\n".encode() + b"".join(o + b"\n" for o in outs))
+    return gen
