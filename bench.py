@@ -298,8 +298,8 @@ def main():
         roof = None
         stp, ffn = prof.get("step"), prof.get("ffn_up")
         # HBM traffic of the same kernel from the committed rocprofv3 PMC passes (FETCH_SIZE and
-        # WRITE_SIZE in separate runs, gfx950 FETCH_SIZE x2 correction): profiles/r01_pmc_traffic.json
-        pmc_file = "r01_pmc_traffic_int8.json" if q8 else "r01_pmc_traffic.json"
+        # WRITE_SIZE in separate runs, gfx950 FETCH_SIZE x2 correction): profiles/r02_pmc_traffic*.json
+        pmc_file = "r02_pmc_traffic_int8.json" if q8 else "r02_pmc_traffic.json"
         pmc = {}
         try:
             with open(os.path.join(REPO, "profiles", pmc_file)) as f:
@@ -316,7 +316,8 @@ def main():
             roof = {"bound": "hbm", "achieved": round(stp["GBps"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(stp["GBps"] / HBM_PEAK_GBS, 4),
                     "traffic": traffic_of("void tl::persistent_step_kernel<"),
-                    "traffic_source": f"profiles/{pmc_file} (rocprofv3 --pmc, positions 0..1)",
+                    "traffic_source": f"profiles/{pmc_file} (rocprofv3 --pmc, mean over the run's launches: "
+                                      "positions 0..255, so ~0.1 GB more K/V than positions 0..15)",
                     "kernel": "persistent_step_kernel (the whole decode step, one launch)",
                     "bytes_per_launch": step_bytes_p, "avg_us": round(stp["avg_us"], 2),
                     "positions": f"0..{P - 1}"}
