@@ -137,7 +137,8 @@ extern "C" int thallama_seqsum_check(const float* in_d, int n, int count, float*
   return (int)e;
 }
 
-// timing of the register form (clock cycles of one call per wave into cyc[count])
+// timing of the register form (clock cycles of one call per wave into cyc[count], low 48 bits;
+// its repair rounds in the bits above)
 __global__ void __launch_bounds__(64) k_seqsum_time(const float* in, int n, float* out, long long* cyc) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const float* a = in + (size_t)blockIdx.x * n;
@@ -146,10 +147,14 @@ __global__ void __launch_bounds__(64) k_seqsum_time(const float* in, int n, floa
   __syncthreads();
   for (int e = threadIdx.x; e < n; e += 64) lds[tl::seqsum_index(e, ch)] = a[e];
   __syncthreads();
+  int rounds[16] = {0};
   const long long t0 = __builtin_amdgcn_s_memtime();
-  const float s = tl::wave_seqsum_reg(lds, n, threadIdx.x);
+  const float s = tl::wave_seqsum_reg(lds, n, threadIdx.x, rounds);
   const long long t1 = __builtin_amdgcn_s_memtime();
-  if (threadIdx.x == 0) { out[blockIdx.x] = s; cyc[blockIdx.x] = t1 - t0; }
+  // cycles in the low 48 bits, repair rounds above
+  if (threadIdx.x == 0) { out[blockIdx.x] = s; cyc[blockIdx.x] = (t1 - t0) | ((long long)rounds[0] << 48); }
+  if (threadIdx.x == 0 && blockIdx.x == 0)  // diagnostics: array 0's failing lane per round
+    for (int k = 1; k < 16; ++k) cyc[gridDim.x + k - 1] = rounds[k];
 }
 
 extern "C" int thallama_seqsum_time(const float* in_d, int n, int count, float* out_d, long long* cyc_d) {

@@ -46,6 +46,11 @@ TL_DEVICE double wave_incl_scan_d(double x) {
   return x;
 }
 
+// Lane l + 1's value (lane 63: 0), by DPP wave_shl:1 (no LDS round trip, unlike __shfl_down).
+TL_DEVICE float wave_next_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xF, 0xF, false));
+}
+
 TL_DEVICE double lane_d(double v, int l) {
   const long long b = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
@@ -105,7 +110,10 @@ TL_DEVICE float wave_seqsum(const float* a, int n, int lane) {
   // guesses from a double prefix of the chunk sums
   float e = chunk_chain(my, ch4, 0.f);
   double inc = (double)e;
-  float start = lane == 0 ? 0.f : (float)(wave_incl_scan_d(inc) - inc);
+  // the scan runs with every lane active (inside the select's lane-0 branch it read lane 0 as
+  // zero: every guess missed chunk 0, and a round was spent per lane the scan fed from lane 0)
+  const double guess = wave_incl_scan_d(inc) - inc;
+  float start = lane == 0 ? 0.f : (float)guess;
   e = chunk_chain(my, ch4, start);
   inc = (double)e - (double)start;
   int lo = 0;
@@ -116,7 +124,7 @@ TL_DEVICE float wave_seqsum(const float* a, int n, int lane) {
     if (lane > lo) start = (float)(base + (incl - incm));
     const float total = (float)(base + lane_d(incl, 63));
     e = chunk_chain(my, ch4, start);
-    float next = __shfl_down(start, 1, 64);
+    float next = wave_next_f(start);
     if (lane == 63) next = total;
     const unsigned long long bad = __ballot(lane >= lo && __float_as_uint(e) != __float_as_uint(next) &&
                                             !(e != e && next != next));
@@ -146,7 +154,7 @@ TL_DEVICE float reg_chain(const f4 (&r)[16], int ch4, float s) {
   return s;
 }
 
-TL_DEVICE float wave_seqsum_reg(const float* a, int n, int lane) {
+TL_DEVICE float wave_seqsum_reg(const float* a, int n, int lane, int* rounds_out = nullptr) {
   const int ch = seqsum_ch(n), ch4 = ch >> 2;
   const f4* my = reinterpret_cast<const f4*>(a + lane * (ch + 4));
   f4 r[16];
@@ -154,7 +162,10 @@ TL_DEVICE float wave_seqsum_reg(const float* a, int n, int lane) {
   for (int k = 0; k < 16; ++k) r[k] = k < ch4 ? my[k] : f4{0.f, 0.f, 0.f, 0.f};
   float e = reg_chain(r, ch4, 0.f);
   double inc = (double)e;
-  float start = lane == 0 ? 0.f : (float)(wave_incl_scan_d(inc) - inc);
+  // the scan runs with every lane active (inside the select's lane-0 branch it read lane 0 as
+  // zero: every guess missed chunk 0, and a round was spent per lane the scan fed from lane 0)
+  const double guess = wave_incl_scan_d(inc) - inc;
+  float start = lane == 0 ? 0.f : (float)guess;
   e = reg_chain(r, ch4, start);
   inc = (double)e - (double)start;
   // one prefix of the guessed increments serves every round: a round re-bases the lanes above
@@ -170,14 +181,21 @@ TL_DEVICE float wave_seqsum_reg(const float* a, int n, int lane) {
     if (lane > lo) start = (float)((double)slo + (pre - plo));
     const float total = round == 0 ? total0 : (float)((double)slo + (lane_d(incl, 63) - plo));
     e = reg_chain(r, ch4, start);
-    float next = __shfl_down(start, 1, 64);
+    float next = wave_next_f(start);
     if (lane == 63) next = total;
     const unsigned long long bad = __ballot(lane >= lo && __float_as_uint(e) != __float_as_uint(next) &&
                                             !(e != e && next != next));
-    if (!bad) return total;
+    if (!bad) {
+      if (rounds_out) *rounds_out = round + 1;
+      return total;
+    }
     const int c = (int)__builtin_ctzll(bad);
     const float ec = lane_f(e, c);
-    if (c == 63) return ec;
+    if (rounds_out && round < 15) rounds_out[1 + round] = c;  // (diagnostics: the failing lane per round)
+    if (c == 63) {
+      if (rounds_out) *rounds_out = round + 1;
+      return ec;
+    }
     lo = c + 1;
     slo = ec;
     plo = lane_d(pre, lo);

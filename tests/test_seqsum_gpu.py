@@ -67,5 +67,7 @@ def test_wave_seqsum_reg_bitexact(gpu, kind, n):
     got = dout.download(np.float32)
     want = np.array([seq_chain(r) for r in a], np.float32)
     np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
-    cyc = dcyc.download(np.int64)
-    print(f"seqsum_reg {kind} n={n}: cycles median {int(np.median(cyc))} max {int(cyc.max())}")
+    raw = dcyc.download(np.int64)
+    cyc, rounds = raw & ((1 << 48) - 1), raw >> 48
+    print(f"seqsum_reg {kind} n={n}: cycles median {int(np.median(cyc))} max {int(cyc.max())}, "
+          f"rounds mean {rounds.mean():.2f} max {int(rounds.max())}")
