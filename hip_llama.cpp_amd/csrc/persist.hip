@@ -607,7 +607,7 @@ TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const flo
       float s;
       if (p.q8 && g.nch > 1) {
         // int8 rows longer than a chunk: runq's chain over the row's group products (runq.c:330-338)
-        s = chain_f4(reinterpret_cast<const f4*>(pbuf + (it * d.rpi + r) * p.pgp), d.K >> 8, 0.f);
+        s = chain_f4<24>(reinterpret_cast<const f4*>(pbuf + (it * d.rpi + r) * p.pgp), d.K >> 8, 0.f);
       } else {
         const float* rr = res + (it * d.rpi + r) * g.nch;
         s = rr[0];
@@ -615,6 +615,9 @@ TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const flo
       }
       v[r] = s;
     }
+    if (p.trace && it == 0)  // (diagnostics: the first item's row values are computed)
+      p.trace[((long long)blockIdx.x * (5 * p.L + 1) + (d.kind == PK_CLS ? 5 * p.L : 5 * l + d.kind)) * kTraceSlots + 12] =
+          __builtin_amdgcn_s_memrealtime();
     const int item = g.i0 + it;
     if (d.kind == PK_CLS) {
       p.logits[item] = v[0];  // read by the host after the launch only

@@ -47,7 +47,7 @@ struct PStep {
 
 constexpr int kPSyncWords = 8 * 32;   // 8 shard counters, one 128-B line each
 constexpr int kPResFloats = 1024;     // per-block row-chunk results (LDS)
-constexpr int kTraceSlots = 12;       // timeline stamps per block and phase (PStep::trace)
+constexpr int kTraceSlots = 16;       // timeline stamps per block and phase (PStep::trace)
 
 // Host: can this step run as one launch on `ncu` co-resident blocks?  Sets pad_floats.
 bool persistent_prepare(PStep& p, int ncu, const char** why);

@@ -46,7 +46,7 @@ def main():
     t = dec.ptrace(False).astype(np.int64)
     L = cfg[2]
     nph = 5 * L + 1
-    NSL = 12  # kTraceSlots (persist.hpp)
+    NSL = 16  # kTraceSlots (persist.hpp)
     G = t.size // (nph * NSL)
     t = t.reshape(G, nph, NSL)
     t = (t - t[:, 0, 0].min()) * 0.01  # us
@@ -115,6 +115,10 @@ def main():
         rel = lambda k: float(np.median((a[:, :, k] - a[:, :, 0])[live]))
         print(f"attention units ({int(live.sum() / len(att))} per layer): q {rel(8):.2f}  scores/kv {rel(9):.2f}  "
               f"summed {rel(11):.2f}  computed {rel(10):.2f}  done {rel(3):.2f} us after phase start")
+    # epilogue: row values computed (slot 12, the control wave's first item) after the epilogue start
+    print("epilogue row values us after its start (median): " + "  ".join(
+        f"{kind} {np.median([np.median(t[:, ph, 12] - t[:, ph, 2]) for ph in range(k, nph - 1, 5)]):.2f}"
+        for kind, k in (("qkv", 0), ("wo", 2), ("ffn_up", 3), ("ffn_down", 4))))
     # epilogue (all slots reduced -> epilogue issued), median and max over blocks
     print("epilogue us (median / max over blocks): " + "  ".join(
         f"{kind} {np.median([np.median(t[:, ph, 3] - t[:, ph, 2]) for ph in range(k, nph - 1, 5)]):.2f}/"
