@@ -57,15 +57,17 @@ TL_DEVICE double lane_d(double v, int l) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-// s = fl(s + x) over the n4 float4s at p (LDS), in order, reading 8 float4 per batch (the
-// compiler waits for all of a batch's LDS reads at the first use: one latency per 32 elements).
+// s = fl(s + x) over the n4 float4s at p (LDS), in order, reading NB float4 per batch (the
+// compiler waits for all of a batch's LDS reads at the first use: one LDS latency per 4 NB
+// elements).
+template <int NB = 8>
 TL_DEVICE float chain_f4(const f4* p, int n4, float s) {
-  for (int j0 = 0; j0 < n4; j0 += 8) {
-    f4 v[8];
+  for (int j0 = 0; j0 < n4; j0 += NB) {
+    f4 v[NB];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = j0 + k < n4 ? p[j0 + k] : f4{0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < NB; ++k) v[k] = j0 + k < n4 ? p[j0 + k] : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
+    for (int k = 0; k < NB; ++k)
       if (j0 + k < n4) {
         s = __fadd_rn(s, v[k].x);
         s = __fadd_rn(s, v[k].y);
