@@ -206,9 +206,19 @@ static void prof_collect(thallama_decoder* d) {
 }
 
 static int auto_splits(const thallama_decoder* d) {
-  // Enough (head, seq, split) blocks to cover the 256 CUs, at most 16 splits.
+  // Enough (head, seq, split) blocks to cover the 256 CUs, at most 16 splits
+  // (THALLAMA_ATTN_SPLITS overrides, for measurements).
+  static const int forced = [] {
+    const char* e = getenv("THALLAMA_ATTN_SPLITS");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced > 0) return forced > 16 ? 16 : forced;
+  // batches aim for 8 waves per CU: a unit walks its keys one 32-key chunk (one memory latency)
+  // after another, so at B = 8 x 32 heads one unit per (b, h) left 256-step decodes latency-bound
+  // (fp32 7B B=8: splits 1 / 2 / 4 / 8 / 16 -> 1366 / 1405 / 1414 / 1417 / 1417 tok/s)
+  const int target = d->B == 1 ? 256 : 2048;
   int blocks = d->H * d->B;
-  int ns = (256 + blocks - 1) / blocks;
+  int ns = (target + blocks - 1) / blocks;
   if (ns < 1) ns = 1;
   if (ns > 16) ns = 16;
   return ns;
