@@ -120,3 +120,28 @@ def test_q8_persistent_bitexact_vs_runq(gpu, oracle, cfg, shared):
             bad = np.flatnonzero(got.view(np.uint32) != want.view(np.uint32))
             raise AssertionError(f"pos {p}: {bad.size} logits differ (first {bad[0]}: {got[bad[0]]!r} vs "
                                  f"{want[bad[0]]!r}, max |d| {np.max(np.abs(got - want)):.3g})")
+
+
+LONG128 = (512, 1536, 2, 4, 2, 1024, 1280)      # head 128, GQA, contexts to 1280 keys
+LONG64 = (512, 1536, 2, 8, 2, 1024, 1100)       # head 64, GQA
+
+
+@pytest.mark.parametrize("cfg", [LONG128, LONG64])
+def test_q8_persistent_bitexact_long_context(gpu, oracle, cfg):
+    """Contexts past one LDS round of the split attention (attention.hpp attn_unit_split): a unit
+    scores at most 64 keys per DMA round (T > 512 keys at 8 units per head) and holds 512 V rows
+    of its columns per round (T > 513), so positions to seq_len exercise the later K and V rounds;
+    teacher-forced logits stay bit-identical to runq's at every position."""
+    oracle.set_threads(16)
+    _, keep, _, dec = q8_decoder(gpu, cfg, 0, 37, 1)
+    assert dec.persistent()
+    ref = oracle.Model(cfg, 0, seed=37)
+    ref.build_q8(64)
+    toks = np.random.default_rng(9).integers(0, cfg[5], cfg[6])
+    for p, t in enumerate(toks):
+        got = dec.forward([int(t)], [p])[0]
+        want = ref.q8_forward(int(t), p)
+        if not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
+            bad = np.flatnonzero(got.view(np.uint32) != want.view(np.uint32))
+            raise AssertionError(f"pos {p}: {bad.size} logits differ (first {bad[0]}: {got[bad[0]]!r} vs "
+                                 f"{want[bad[0]]!r}, max |d| {np.max(np.abs(got - want)):.3g})")
