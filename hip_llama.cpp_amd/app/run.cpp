@@ -134,11 +134,14 @@ struct Replica {
 };
 
 // Weights on every device: one H2D copy to device 0, then an RCCL broadcast (in 1 GiB
-// pieces) into every other device's arena.
-static std::vector<Replica> replicate(ModelFile& m, int n_dev, int batch) {
-  std::vector<Replica> reps((size_t)n_dev);
-  for (int d = 0; d < n_dev; ++d) {
-    HIP_OK(hipSetDevice(d));
+// pieces) into every other device's arena.  n_rep > n_dev (THALLAMA_REPLICAS, a rehearsal of the
+// multi-GPU worker split on fewer GPUs): replica r lives on device r % n_dev and the replicas
+// past the first n_dev get their weights by a device-to-device copy.
+static std::vector<Replica> replicate(ModelFile& m, int n_dev, int n_rep, int batch) {
+  std::vector<Replica> reps((size_t)n_rep);
+  for (int d = 0; d < n_rep; ++d) {
+    reps[d].dev = d % n_dev;
+    HIP_OK(hipSetDevice(reps[d].dev));
     HIP_OK(hipMalloc(&reps[d].arena, m.bytes));
   }
   HIP_OK(hipSetDevice(0));
@@ -169,10 +172,13 @@ static std::vector<Replica> replicate(ModelFile& m, int n_dev, int batch) {
       ncclCommDestroy(comms[d]);
     }
   }
-  for (int d = 0; d < n_dev; ++d) {
-    HIP_OK(hipSetDevice(d));
+  for (int d = n_dev; d < n_rep; ++d) {
+    HIP_OK(hipSetDevice(reps[d].dev));
+    HIP_OK(hipMemcpy(reps[d].arena, reps[reps[d].dev].arena, m.bytes, hipMemcpyDeviceToDevice));
+  }
+  for (int d = 0; d < n_rep; ++d) {
     Replica& r = reps[d];
-    r.dev = d;
+    HIP_OK(hipSetDevice(r.dev));
     alloc_state_to_device_batch(&m.t, r.s, batch);
     int rc;
     if (m.q8) {
@@ -336,7 +342,7 @@ int main(int argc, char* argv[]) {
   thallama_sampler* smp = thallama_sampler_create(V, temperature, topp, rng_seed);
 
   if (strcmp(mode, "generate") == 0) {
-    std::vector<Replica> reps = replicate(model, 1, 1);
+    std::vector<Replica> reps = replicate(model, 1, 1, 1);
     generate(model.cfg, reps[0], tok, smp, prompt, steps);
     release(reps);
   } else if (strcmp(mode, "chat") == 0) {
@@ -356,17 +362,21 @@ int main(int argc, char* argv[]) {
            (unsigned long)(((size_t)thallama_requests_count(req) * max_token_len * steps + 1) * 2));
     int n_dev = 0;
     HIP_OK(hipGetDeviceCount(&n_dev));
+    // one worker (replica) per GPU like the reference; THALLAMA_REPLICAS=N runs N workers over
+    // the GPUs there are (a rehearsal of an N-GPU run: the worker split, the per-replica decoders)
+    const char* rep_env = getenv("THALLAMA_REPLICAS");
+    const int n_rep = rep_env && atoi(rep_env) > 0 ? atoi(rep_env) : n_dev;
     fprintf(stderr, "\n DATA PARALLELISM \n");
-    fprintf(stderr, "\n Num Devices %d\n", n_dev);
+    fprintf(stderr, "\n Num Devices %d\n", n_rep);
     fprintf(stderr, "\n Batch Size %d\n", batch);
     const long load_start = time_in_ms();
-    std::vector<Replica> reps = replicate(model, n_dev, batch);
+    std::vector<Replica> reps = replicate(model, n_dev, n_rep, batch);
     fprintf(stdout, "\nLoad model time (1 upload + RCCL broadcast to %d GPUs): %f\n", n_dev,
             (double)(time_in_ms() - load_start) / 1000);
 
     const long start = time_in_ms();
     long long num_gen_tokens = 0;
-    const int st = thallama_serve_requests_prefill(req, tokenizer_path, V, n_dev, batch, replica_step, replica_prefill,
+    const int st = thallama_serve_requests_prefill(req, tokenizer_path, V, n_rep, batch, replica_step, replica_prefill,
                                                    &reps, &num_gen_tokens);
     const long end = time_in_ms();
     if (st != 0) {

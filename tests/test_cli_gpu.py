@@ -90,6 +90,24 @@ def test_test_mode_output_file_byte_identical(gpu, host, model, tmp_path, batch,
     assert f"Total achieved token: {gen}".encode() in r.stdout
 
 
+@pytest.mark.parametrize("batch", [1, 3])
+def test_test_mode_worker_split_replicas(gpu, host, model, tmp_path, batch):
+    """The CLI's multi-GPU form (src/llama.cpp:891-1083: one worker per GPU, each with its own
+    replica and decoder, requests dealt from one shared counter), rehearsed on this GPU with
+    THALLAMA_REPLICAS=3 (three workers and replicas on one device, weights copied device to
+    device): the output file and the token count are those of the single-worker run."""
+    ref, path = model
+    inp = tmp_path / "in.txt"
+    inp.write_bytes((f"{len(PROMPTS)}\n" + "\n".join(PROMPTS) + "\n").encode())
+    out = tmp_path / "out.txt"
+    r = run_cli([path, "-m", "test", "-f", str(inp), "-o", str(out), "-b", str(batch), "-z", TOK], tmp_path,
+                env={"THALLAMA_REPLICAS": "3"})
+    assert b"Num Devices 3" in r.stderr
+    want, gen = expected_test_mode(host, ref, PROMPTS, CFG[6])
+    assert out.read_bytes() == f"{len(PROMPTS)}\n".encode() + b"".join(w + b"\n" for w in want)
+    assert f"Total achieved token: {gen}".encode() in r.stdout
+
+
 def test_test_mode_greedy_flag(gpu, host, model, tmp_path):
     """-g 1 (an addition): test mode decodes greedily; every output is the CPU oracle's greedy
     continuation of its prompt (src/seq.cpp forward, argmax with the lowest index on ties)."""
