@@ -49,6 +49,7 @@ def main():
     NSL = 16  # kTraceSlots (persist.hpp)
     G = t.size // (nph * NSL)
     t = t.reshape(G, nph, NSL)
+    raw = t.copy()  # (slot 13 holds a count, not a time)
     t = (t - t[:, 0, 0].min()) * 0.01  # us
     dim, hid, kvd, V = cfg[0], cfg[1], cfg[0] * cfg[4] // cfg[3], cfg[5]
     esz = 4 if args.dtype == "f32" else 1 + 4 / 64  # int8 + one fp32 scale per 64
@@ -115,6 +116,12 @@ def main():
         rel = lambda k: float(np.median((a[:, :, k] - a[:, :, 0])[live]))
         print(f"attention units ({int(live.sum() / len(att))} per layer): q {rel(8):.2f}  scores/kv {rel(9):.2f}  "
               f"summed {rel(11):.2f}  computed {rel(10):.2f}  done {rel(3):.2f} us after phase start")
+    # int8: repair rounds of the exact norm sums (slot 13, seqsum.hpp)
+    if args.dtype == "int8":
+        print("norm-sum repair rounds (mean / max over blocks and layers): " + "  ".join(
+            f"{kind} {np.mean([raw[:, ph, 13] for ph in range(k, nph - 1, 5)]):.2f}/"
+            f"{np.max([raw[:, ph, 13] for ph in range(k, nph - 1, 5)])}"
+            for kind, k in (("qkv", 0), ("ffn_up", 3))))
     # epilogue: row values computed (slot 12, the control wave's first item) after the epilogue start
     print("epilogue row values us after its start (median): " + "  ".join(
         f"{kind} {np.median([np.median(t[:, ph, 12] - t[:, ph, 2]) for ph in range(k, nph - 1, 5)]):.2f}"
