@@ -4,6 +4,7 @@
 #include <stdlib.h>
 #include "gemv_dispatch.hpp"
 #include "gemv_mfma.hpp"
+#include "gemv_rr.hpp"
 
 namespace tl {
 
@@ -28,6 +29,40 @@ inline void mfma_splits(GemvParams& p, int tiles) {
   if (ms < 1) ms = 1;
   p.msteps = (nsteps + ms - 1) / ms;
   p.msplit = (nsteps + p.msteps - 1) / p.msteps;
+}
+
+// The register-resident batched GEMV (gemv_rr.hpp) when the rows fill every CU and a block's rows
+// fit its LDS partials, for up to rr_max_nb() sequences: 4 by default (7B fp32 B=4: 740 vs 726
+// tok/s on the matrix-core kernel; at 8 sequences it measured slower, 1255-1328 vs 1408-1433,
+// tools/job_r02_t.sh), env THALLAMA_GEMV_RR=N moves the bound (0 = never).  Same ssq contract
+// as the matrix-core kernel, so the two mix freely within a step.
+inline int rr_max_nb() {
+  static const int v = [] {
+    const char* e = getenv("THALLAMA_GEMV_RR");
+    return e ? atoi(e) : 4;
+  }();
+  return v;
+}
+
+inline int rr_grid() {
+  static const int v = [] {
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    return ncu;
+  }();
+  return v;
+}
+
+template <int MODE>
+inline bool rr_ok(const GemvParams& p) {
+  const int G = rr_grid();
+  if (p.nb > rr_max_nb() || p.nb > 8 || (p.K & 255) || (p.x_stride & 3)) return false;
+  constexpr int RPI = RowsPerItem<MODE>::v;
+  const long long rows = (long long)p.n_items * RPI;
+  if (rows < 16LL * G) return false;
+  const int per = MODE == GM_RESID ? 16 * (((p.n_items + 15) / 16 + G - 1) / G)
+                                   : (p.n_items + G - 1) / G * RPI;
+  return per <= kRrMaxRows;
 }
 
 template <int MODE, int NB, int IPW, bool NT, int WAVES, bool PF>
@@ -112,6 +147,14 @@ inline hipError_t launch_mode(const GemvParams& p0, hipStream_t s, const GemvCfg
         p.rms_w = nullptr;
         p.tok = nullptr;
         p.x_out = nullptr;
+      }
+      if (rr_ok<MODE>(p)) {
+        const dim3 g(rr_grid()), b(kRrWaves * 64);
+        if (p.nb <= 4) hipLaunchKernelGGL((gemv_rr_kernel<MODE, 4, 2, 4>), g, b, 0, s, p);
+        else hipLaunchKernelGGL((gemv_rr_kernel<MODE, 8, 2, 4>), g, b, 0, s, p);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        continue;
       }
       const int rows = MODE == GM_QKV ? 2 * p.n_items : p.n_items;
       const int tiles = (rows + 15) / 16;

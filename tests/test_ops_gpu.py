@@ -152,6 +152,26 @@ def test_matmul_batch_offsets(gpu, handle, oracle, B):
     np.testing.assert_array_equal(got[untouched], 7.0)
 
 
+@pytest.mark.parametrize("B", [4, 5, 8])
+@pytest.mark.parametrize("M,K", [(4096, 4096), (4096, 11008), (12288, 2048)])
+def test_matmul_batch_register_resident(gpu, handle, oracle, M, K, B):
+    """Batched GEMV at 7B row counts: B = 4 takes the register-resident kernel (gemv_rr.hpp; K =
+    11008 is three passes of 16 / 16 / 11 chunks, the last pass leaves waves idle), B = 5 and 8 the
+    matrix-core kernel (the register-resident one with THALLAMA_GEMV_RR=8); 1e-4 vs the oracle."""
+    r = rng(M + K + B)
+    W = (r.standard_normal((M, K)) * 0.02).astype(np.float32)
+    X = r.standard_normal((B, K)).astype(np.float32)
+    pos = np.zeros(B, np.int32)
+    C0 = np.full(B * M, 7.0, np.float32)
+    dW, dX, dC, dpos = dev(gpu, W), dev(gpu, X), dev(gpu, C0), dev(gpu, pos)
+    assert gpu.lib().thaBLAS_s_matmul_batch(C.byref(handle), B, dC.fptr(), dX.fptr(), dW.fptr(), K, M, 0, 0,
+                                            dpos.iptr(), M, K) == 0
+    gpu.sync()
+    got = dC.download().reshape(B, M)
+    for b in range(B):
+        assert_ref_close(got[b], oracle.matmul(W, X[b]), 1e-4, f"rr gemv {M}x{K} b={b}")
+
+
 @pytest.mark.parametrize("m,n,k", [(3, 3, 3), (100, 100, 100), (1000, 1000, 1000), (65, 130, 33)])
 def test_sgemm(gpu, handle, m, n, k):
     r = rng(m + n + k)
