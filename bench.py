@@ -60,6 +60,8 @@ def main():
     ap.add_argument("--device-map", default="", help="comma list: local rank -> HIP device (rehearsals that "
                                                      "put several ranks on one GPU)")
     args = ap.parse_args()
+    if args.prof_steps < 1:
+        ap.error("--prof-steps must be >= 1 (the roofline object times the dominant kernel over them)")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -213,7 +215,7 @@ def main():
     # (the persistent step is ONE launch: class "step"; the multi-launch kernels are profiled
     # as well for the breakdown, with the persistent path switched off)
     prof, prof_ml = {}, {}
-    P = min(args.prof_steps, K)
+    P = min(args.prof_steps, K)  # >= 1 (argument check): the roofline needs a measured kernel
     step_bytes_p = sum(launch_bytes(tl.K_STEP, [p] * B) for p in range(P)) / P
 
     def profile(into):

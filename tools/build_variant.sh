@@ -5,7 +5,7 @@ set -e
 cd "$(dirname "$0")/../hip_llama.cpp_amd"
 name=$1; shift
 mkdir -p /tmp/variants
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -Wall -Wno-unused-function \
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -ffp-contract=off -Wall -Wno-unused-function \
   -I../include $* -c csrc/persist.hip -o /tmp/variants/persist_$name.o
 objs=$(ls build/*.o | grep -v '/persist.o')
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o lib/libthallama.so.$name $objs /tmp/variants/persist_$name.o
