@@ -19,7 +19,7 @@
 //  * the wave then sweeps every row of its block: one 1-KiB nt wave-load per row and chunk
 //    (two batches of RB rows in flight), v_pk_fma_f32 into acc[row][seq pair];
 //  * per batch the RB*NB lane partials are reduced by recursive halving (each exchange
-//    step halves the values a lane carries: shfl 32/16, then DPP row_mirror,
+//    step halves the values a lane carries: v_permlane32/16_swap, then DPP row_mirror,
 //    row_half_mirror, quad_perm), so the 64-lane sums cost ~2 VALU per value, and land in
 //    LDS as [wave][row][seq];
 //  * at the end of a pass the 8 wave partials are added in wave order; K > 8*CPW chunks
@@ -51,7 +51,20 @@ template <int D, int M>
 TL_DEVICE void rr_stage(float (&v)[M], int lane) {
   if constexpr (D >= 1) {
     const bool hi = (lane & D) != 0;
-    if constexpr (M >= 2) {
+    if constexpr (M >= 2 && (D == 32 || D == 16)) {
+      // gfx950 v_permlane{32,16}_swap: odd rows (of D lanes) of a trade places with even rows of
+      // b, so a' + b' holds a's pair sums in the even rows and b's in the odd ones (VALU only)
+#pragma unroll
+      for (int j = 0; j < M / 2; ++j) {
+        const unsigned a = __float_as_uint(v[j]), b = __float_as_uint(v[j + M / 2]);
+        const auto r = D == 32 ? __builtin_amdgcn_permlane32_swap(a, b, false, false)
+                               : __builtin_amdgcn_permlane16_swap(a, b, false, false);
+        v[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+      }
+      (void)hi;
+      float (&h)[M / 2] = *reinterpret_cast<float(*)[M / 2]>(&v[0]);
+      rr_stage<D / 2, M / 2>(h, lane);
+    } else if constexpr (M >= 2) {
 #pragma unroll
       for (int j = 0; j < M / 2; ++j) {
         const float send = hi ? v[j] : v[j + M / 2];
