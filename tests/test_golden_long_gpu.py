@@ -15,7 +15,8 @@ be no further from the CPU reference than the reference's own GPU implementation
 the count beyond 1e-4), every earlier token still identical; the 110M cases keep 1e-4.
 Cases: stories110M shape with a shared and an unshared classifier, and llama2-7B (the bench's own
 model: same seed), each on the persistent one-launch step, the multi-launch step, and — for the
-8-GPU config's per-GPU workload — 8 sequences at once on the matrix-core GEMV path.
+8-GPU config's per-GPU workload — 8 sequences at once on the matrix-core GEMV path, and 4 at once
+(at 7B the register-resident GEMV, gemv_rr.hpp).
 """
 import json
 import os
@@ -44,11 +45,11 @@ def fp32_decoder(tl, case, batch):
 
 
 @pytest.mark.parametrize("name", ["stories110m_shared", "stories110m_unshared", "llama2_7b"])
-@pytest.mark.parametrize("path", ["persistent", "multilaunch", "batch8"])
+@pytest.mark.parametrize("path", ["persistent", "multilaunch", "batch8", "batch4"])
 def test_fp32_256_step_greedy_equals_reference(gpu, name, path):
     case = CASES[name]
     g = case["fp32"]
-    B = 8 if path == "batch8" else 1
+    B = {"batch8": 8, "batch4": 4}.get(path, 1)
     keep, dec = fp32_decoder(gpu, case, B)
     dec.set(gpu.OPT_USE_GRAPH, 1)
     if path == "multilaunch":
