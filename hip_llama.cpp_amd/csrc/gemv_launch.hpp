@@ -21,9 +21,12 @@ inline int gemv_mfma_min_nb() {
 // Split K across blocks when the row tiles alone leave CUs idle: msplit = target / tiles,
 // at least 2 steps per wave per split; needs the decoder's mpart/mcnt scratch, sized for
 // mfma_target_blocks() tiles x splits.
-inline void mfma_splits(GemvParams& p, int tiles) {
+// depth2: aim for half the blocks (the residual launch with K <= 4096, i.e. Wo: in the 7B B=8 step
+// 18.3 us at 2 blocks per CU against 19.9-20.3 at 3-4; W2, QKV and W1/W3 keep 4, and 6-8 lost
+// everywhere: tools/job_r02_depth.sh).
+inline void mfma_splits(GemvParams& p, int tiles, bool depth2 = false) {
   const int nsteps = p.K >> 4;
-  int ms = p.mpart && p.mcnt ? mfma_target_blocks() / tiles : 1;
+  int ms = p.mpart && p.mcnt ? mfma_target_blocks() / (depth2 && !getenv("THALLAMA_MFMA_DEPTH") ? 2 : 1) / tiles : 1;
   const int cap = nsteps / (2 * kMfmaWaves);
   if (ms > cap) ms = cap;
   if (ms < 1) ms = 1;
@@ -158,7 +161,7 @@ inline hipError_t launch_mode(const GemvParams& p0, hipStream_t s, const GemvCfg
       }
       const int rows = MODE == GM_QKV ? 2 * p.n_items : p.n_items;
       const int tiles = (rows + 15) / 16;
-      mfma_splits(p, tiles);
+      mfma_splits(p, tiles, MODE == GM_RESID && p.K <= 4096);
       const dim3 grid(tiles * p.msplit);
       // activation load instructions per 16-row group (4 rows each): only those with live rows
       const dim3 blk(kMfmaWaves * 64);
