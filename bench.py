@@ -1,22 +1,38 @@
 #!/usr/bin/env python3
 """bench.py — decode tokens/s + achieved HBM GB/s on MI355X (BASELINE.json metric).
 
-One "step" = one greedy decode token for the B sequences a GPU holds, running the whole
-thaDNN forward (all layers, classifier, on-device argmax feeding the next token).
-Default workload (the N=1 line): llama2-7B-shaped fp32 model, random-init synthetic weights,
-one BOS-started greedy sequence per GPU over positions 0..K-1 (BASELINE.json configs[2]).
-Other configs: --dtype int8 (configs[3], runq Q8_0 layout), --batch 8 (configs[4] per GPU),
---model 110m (configs[1]).
-Multi-GPU: one process per GPU (torch.distributed.run); each rank decodes its own
-independent sequences (weak scaling, no collective on the data path); rank 0 synthesises the
-weights once and RCCL-broadcasts them over xGMI.
+Workloads (one "step" = one pass of the hot path over one batch of synthetic input):
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--model 7b|110m] [--dtype f32|int8] [--batch B]
+* ``decode`` (default at N = 1; BASELINE.json configs[2], or [3] with --dtype int8, [1] with
+  --model 110m): a step is one 256-token greedy decode (--decode-len) of the B sequences a GPU
+  holds, BOS-started at position 0 and run to position 255 — every step the whole thaDNN forward
+  (all layers, classifier, on-device argmax feeding the next token).  value = tokens/s over the
+  K timed decodes.  The line also carries the long-context tail (positions 1792..2047 of a
+  2048-token decode, the length the reference's test mode runs to), the 1-GPU point of the
+  request workload below, the dominant kernel's roofline and the CPU baseline.
+* ``requests`` (default at N > 1; BASELINE.json configs[4]): the reference's test mode
+  (src/llama.cpp:891-1083) over its assets/in/gen_in_64.txt prompts — 8 prompts per GPU
+  (--prompts-per-gpu; all 64 at N = 8), 8 slots per GPU, greedy, prompt prefilled, each request
+  decoded to position 255 or EOS/BOS.  A step is one pass over the job; value = the reference's
+  token count (sum of pos - 1 over requests, src/llama.cpp:1062) / time, max over ranks.  The
+  output file rank 0 gathers is compared with a committed one-process fixture.
+
+Multi-GPU: one process per GPU.  ``--gpus N`` with no WORLD_SIZE in the environment starts the N
+ranks itself (torch.distributed.run as a child process, before anything touches a GPU) and exits
+with their status; under an outer torch.distributed.run it is one rank.  Rank 0 synthesises the
+weights once and RCCL-broadcasts them over xGMI; no collective on the data path (weak scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload decode|requests]
+                    [--model 7b|110m] [--dtype f32|int8] [--batch B]
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -29,26 +45,37 @@ MODELS = {
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 SEED = 20240224
+GOLDEN = os.path.join(REPO, "tests", "golden")
+PROMPTS = os.path.join(GOLDEN, "gen_in_64.txt")  # the reference's assets/in/gen_in_64.txt
+TOKENIZER = os.path.join(GOLDEN, "tokenizer.bin")  # the reference's assets/tokenizer.bin
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def main():
+def parse_args(argv):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=256)
-    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=5, help="timed steps (decodes / request passes)")
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", choices=["decode", "requests"], default=None,
+                    help="default: decode at N = 1, requests at N > 1")
+    ap.add_argument("--decode-len", type=int, default=256, help="positions per sequence (configs[2]: 256)")
     ap.add_argument("--model", default="7b", choices=sorted(MODELS))
     ap.add_argument("--dtype", default="f32", choices=["f32", "int8"])
     ap.add_argument("--group-size", type=int, default=64, help="Q8_0 group size (int8)")
-    ap.add_argument("--batch", type=int, default=1, help="sequences per GPU")
+    ap.add_argument("--batch", type=int, default=0, help="sequences (slots) per GPU; default 1 decode, 8 requests")
+    ap.add_argument("--prompts-per-gpu", type=int, default=8)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-nt", action="store_true")
     ap.add_argument("--splits", type=int, default=0)
     ap.add_argument("--no-persistent", action="store_true",
-                    help="multi-launch step instead of the one-launch persistent step (batch 1)")
+                    help="multi-launch step instead of the one-launch persistent step")
+    ap.add_argument("--no-long", action="store_true", help="skip the positions 1792..2047 line")
+    ap.add_argument("--no-requests-point", action="store_true", help="skip the 1-GPU request-workload point")
+    ap.add_argument("--write-fixture", action="store_true",
+                    help="requests: serve all 64 prompts in this process and write the output fixture")
     ap.add_argument("--cpu-baseline-tokens", type=int, default=0,
                     help="greedy tokens the CPU baseline decodes (0: as many as fit --cpu-baseline-seconds)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
@@ -59,20 +86,117 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (CPU rehearsal)")
     ap.add_argument("--device-map", default="", help="comma list: local rank -> HIP device (rehearsals that "
                                                      "put several ranks on one GPU)")
-    args = ap.parse_args()
+    ap.add_argument("--plumbing", action="store_true",
+                    help="no GPU: ranks, sharding and output gathering over a deterministic CPU step (tests)")
+    args = ap.parse_args(argv)
     if args.prof_steps < 1:
         ap.error("--prof-steps must be >= 1 (the roofline object times the dominant kernel over them)")
+    if args.gpus < 1 or args.steps < 1 or args.warmup < 0:
+        ap.error("--gpus and --steps must be >= 1, --warmup >= 0")
+    return args
 
+
+def launch_ranks(args, argv):
+    """--gpus N > 1 without WORLD_SIZE: one rank per GPU via torch.distributed.run, started as a CHILD
+    process (nothing here has touched a GPU); returns its exit status."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    log(f"bench.py: starting {args.gpus} ranks: {' '.join(cmd[1:8])} ...")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def read_prompts(path, n):
+    """The first n prompts of a reference request file (read_inputfile, src/llama.cpp:424-453)."""
+    from hip_llama_cpp_amd import host as H
+    r = H.Requests(path, 512, 1024)
+    if n > len(r):
+        raise SystemExit(f"{n} prompts requested, {path} holds {len(r)}")
+    return [r.prompt(i) for i in range(n)]
+
+
+def write_requests(prompts, d):
+    fd, path = tempfile.mkstemp(prefix=".bench_req_", suffix=".txt", dir=d)
+    with os.fdopen(fd, "wb") as f:
+        f.write(f"{len(prompts)}\n".encode() + b"".join(p + b"\n" for p in prompts))
+    return path
+
+
+def sha(strings):
+    return hashlib.sha256("\x00".join(strings).encode()).hexdigest()[:16]
+
+
+# ---------------------------------------------------------------- --plumbing (CPU only, tests)
+def plumbing(args, world, rank):
+    """Everything of the request workload except the GPU: rank start-up, prompt sharding, the
+    reference scheduler, gathering on rank 0.  The step is a deterministic function of
+    (token, pos) — a peaked one-hot — so outputs are comparable across world sizes."""
+    import numpy as np
+    import torch.distributed as dist
+    from hip_llama_cpp_amd import dist as D
+    if world > 1:
+        dist.init_process_group(backend="gloo")
+    V = 32000
+
+    def step(_w, tok, pos):
+        lg = np.zeros((len(tok), V), np.float32)
+        for b, (t, p) in enumerate(zip(tok, pos)):
+            lg[b, (int(t) * 7919 + int(p) * 104729 + 13) % (V - 3) + 3] = 1.0
+        return lg
+    n = args.prompts_per_gpu * world
+    wd = tempfile.mkdtemp(prefix=".bench_", dir=REPO)
+    req = write_requests(read_prompts(PROMPTS, n), wd) if rank == 0 else None
+    if world > 1:
+        box = [req]
+        dist.broadcast_object_list(box, src=0)
+        req = box[0]
+    out = os.path.join(wd, "out.txt")
+    outs = []
+    t = time.perf_counter()
+    gen = D.serve_sharded(req, out, TOKENIZER, V, args.batch or 8, step, 64, args.decode_len, temperature=0.0,
+                          workdir=wd, outputs=outs)
+    el = D.max_over_ranks(time.perf_counter() - t)
+    if world > 1:
+        dist.barrier()
+    if rank == 0:
+        outs = [o.decode("utf-8", "replace") for o in outs]
+        print(json.dumps({"metric": "plumbing (no GPU)", "plumbing": True, "n_gpus": world, "ranks": world,
+                          "prompts": n, "tokens": gen, "seconds": round(el, 3),
+                          "outputs_sha": [hashlib.sha256(o.encode()).hexdigest()[:12] for o in outs]}), flush=True)
+        os.remove(out)
+        os.remove(req)
+        os.rmdir(wd)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------- GPU
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"bench.py: --gpus {args.gpus} but {world} rank(s) were started")
+        sys.exit(3)
+    from __graft_entry__ import _pkg
+    _pkg()
+    if args.plumbing:
+        return plumbing(args, world, rank)
     if args.device_map:
         local = [int(v) for v in args.device_map.split(",")][local]
+    workload = args.workload or ("decode" if world == 1 else "requests")
 
     import torch
     import torch.distributed as dist
-    from __graft_entry__ import _pkg
-    _pkg()
     from hip_llama_cpp_amd import thallama as tl
     from hip_llama_cpp_amd import dist as D
 
@@ -89,15 +213,15 @@ def main():
 
     cfg_t, shared, mname = MODELS[args.model]
     c = tl.Config.make(*cfg_t)
-    B, K, W = args.batch, args.steps, args.warmup
     S, L = cfg_t[6], cfg_t[2]
     gs = args.group_size
-    if K > S or W > S:
-        raise SystemExit(f"--steps/--warmup must be <= seq_len {S}")
     q8 = args.dtype == "int8"
+    T = args.decode_len
+    if T > S or T < 2:
+        raise SystemExit(f"--decode-len must be in [2, seq_len {S}]")
 
-    # ---------------- weights: rank 0 synthesises (and for int8 quantises, export.py
-    # semantics), then one RCCL broadcast of the packed weight image to every other rank
+    # ---------------- weights: rank 0 synthesises (and for int8 quantises, export.py semantics),
+    # then one RCCL broadcast of the packed weight image to every other rank
     t0 = time.perf_counter()
     n_floats = tl.lib().thallama_v0_payload_floats(tl.C.byref(c), shared)
     if not q8:
@@ -127,232 +251,366 @@ def main():
         torch.cuda.synchronize()
         t_bcast = time.perf_counter() - tb
     t_init = time.perf_counter() - t0
-    if q8:
-        model = tl.DeviceModelQ8(c, shared, gs, payload_ptr=image.data_ptr())
-    else:
-        model = tl.DeviceModel(c, shared, arena_ptr=image.data_ptr())
-    state = tl.DeviceState(c, B)
-    dec = tl.Decoder(model, state)
-    dec.set(tl.OPT_USE_GRAPH, 0 if args.no_graph else 1)
-    if args.no_nt:
-        dec.set(tl.OPT_NT_WEIGHTS, 0)
-    if args.splits:
-        dec.set(tl.OPT_ATTN_SPLITS, args.splits)
-    if args.no_persistent:
-        dec.set(tl.OPT_PERSISTENT, 0)
-    persistent = dec.persistent()
-    log(f"[rank {rank}] {mname} {args.dtype} B={B} init {t_init:.2f}s (broadcast {t_bcast:.2f}s)")
+    model = (tl.DeviceModelQ8(c, shared, gs, payload_ptr=image.data_ptr()) if q8
+             else tl.DeviceModel(c, shared, arena_ptr=image.data_ptr()))
 
-    tok0, pos0 = [1] * B, [0] * B  # BOS at position 0
-    if W:
-        dec.greedy(tok0, pos0, W, want_tokens=False, sync=True)
+    def make_decoder(B):
+        state = tl.DeviceState(c, B)
+        dec = tl.Decoder(model, state)
+        dec.set(tl.OPT_USE_GRAPH, 0 if args.no_graph else 1)
+        if args.no_nt:
+            dec.set(tl.OPT_NT_WEIGHTS, 0)
+        if args.splits:
+            dec.set(tl.OPT_ATTN_SPLITS, args.splits)
+        if args.no_persistent:
+            dec.set(tl.OPT_PERSISTENT, 0)
+        return state, dec
 
-    def timed(n):
-        """n greedy steps at positions 0..n-1, barrier + synchronize on both sides, max over ranks"""
+    def launch_bytes(B, kclass, pos):
+        return tl.step_bytes_q8(c, B, kclass, pos, gs) if q8 else tl.step_bytes(c, B, kclass, pos)
+
+    layer_classes = (tl.K_QKV, tl.K_ATTN, tl.K_WO, tl.K_FFN_UP, tl.K_FFN_DOWN)
+
+    def token_bytes(B, p):
+        """Algorithmic bytes of one greedy step of B sequences at position p: weights once, K/V rows."""
+        return (L * sum(launch_bytes(B, k, [p] * B) for k in layer_classes) + launch_bytes(B, tl.K_CLS, [p] * B)
+                + launch_bytes(B, tl.K_ARGMAX, [p] * B))
+
+    def timed(fn, n):
+        """n calls of fn, barrier + synchronize on both sides, max over ranks"""
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t = time.perf_counter()
-        dec.greedy(tok0, pos0, n, want_tokens=False, sync=True)
+        for _ in range(n):
+            fn()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         return D.max_over_ranks(time.perf_counter() - t, device=dev)
 
-    # ---------------- timed region: K greedy steps at positions 0..K-1
-    elapsed = timed(K)
-    value = world * B * K / elapsed
-    ms_step = elapsed / K * 1e3
-    # the persistent step gives up (and the call re-runs on the multi-launch path) only if its
-    # grid was not co-resident: re-read the path after the timed region, report any fallback
-    persistent_after = dec.persistent()
-    # BASELINE.json configs[2]: the 256-token decode (positions 0..255), timed in the same run
-    # whatever --steps is (about 1.1 s at 7B fp32)
-    HEAD = 256
-    elapsed_h = elapsed if K == HEAD else (timed(HEAD) if S >= HEAD else None)
-    persistent_after = persistent_after and dec.persistent()
+    def profile_roofline(dec, B):
+        """Per-kernel-class HIP events on the decoder's stream over an eager replay of the first
+        prof-steps positions; the dominant kernel's roofline object."""
+        prof, prof_ml = {}, {}
+        P = min(args.prof_steps, T)
+        persistent = dec.persistent()
+        step_bytes_p = sum(launch_bytes(B, tl.K_STEP, [p] * B) for p in range(P)) / P
 
-    # ---------------- algorithmic bytes per step: weights once + KV rows at each position
-    def launch_bytes(kclass, pos):
-        return tl.step_bytes_q8(c, B, kclass, pos, gs) if q8 else tl.step_bytes(c, B, kclass, pos)
-
-    layer_classes = (tl.K_QKV, tl.K_ATTN, tl.K_WO, tl.K_FFN_UP, tl.K_FFN_DOWN)
-    step_bytes = sum(L * sum(launch_bytes(k, [p] * B) for k in layer_classes) + launch_bytes(tl.K_CLS, [p] * B)
-                     + launch_bytes(tl.K_ARGMAX, [p] * B) for p in range(K)) / K
-    step_gbs = step_bytes / (ms_step * 1e-3) / 1e9
-    headline = None
-    if elapsed_h is not None:
-        hb = sum(L * sum(launch_bytes(k, [p] * B) for k in layer_classes) + launch_bytes(tl.K_CLS, [p] * B)
-                 + launch_bytes(tl.K_ARGMAX, [p] * B) for p in range(HEAD)) / HEAD
-        hms = elapsed_h / HEAD * 1e3
-        headline = {"workload": f"{mname} {args.dtype} {HEAD}-token greedy decode (BASELINE.json configs), "
-                                f"{B} seq/GPU, positions 0..{HEAD - 1}",
-                    "value": round(world * B * HEAD / elapsed_h, 3), "unit": "tok/s", "ms_per_step": round(hms, 4),
-                    "achieved_GBps": round(hb / (hms * 1e-3) / 1e9, 1),
-                    "frac_of_peak": round(hb / (hms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                    "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / hb * B * world, 1)}
-
-    # ---------------- greedy tokens vs the reference's own 256-step decode (tests/golden/
-    # reference_long.json, generated from the reference's seq.cpp / runq.c by make_golden_long.py)
-    golden = None
-    try:
-        with open(os.path.join(REPO, "tests", "golden", "reference_long.json")) as f:
-            gcases = json.load(f)["cases"]
-    except (OSError, ValueError, KeyError):
-        gcases = []
-    for gc in gcases:
-        if tuple(gc["config"]) == tuple(cfg_t) and gc["shared"] == shared and gc["seed"] == SEED:
-            want = gc["q8" if q8 else "fp32"]["tokens"]
-            got = dec.greedy(tok0, pos0, len(want))  # [steps][B]
-            prefix = min(next((i for i, (a, b) in enumerate(zip(want, got[:, b].tolist())) if a != b), len(want))
-                         for b in range(B))
-            golden = {"steps": len(want), "tokens_match": prefix == len(want), "match_prefix": prefix,
-                      "source": "tests/golden/reference_long.json (" + ("runq.c" if q8 else "src/seq.cpp") +
-                                " compiled from the reference, greedy from BOS)"}
-
-    # ---------------- per-kernel-class timing: HIP events around every launch on the decoder's
-    # stream, over an eager replay of the first prof-steps positions
-    # (the persistent step is ONE launch: class "step"; the multi-launch kernels are profiled
-    # as well for the breakdown, with the persistent path switched off)
-    prof, prof_ml = {}, {}
-    P = min(args.prof_steps, K)  # >= 1 (argument check): the roofline needs a measured kernel
-    step_bytes_p = sum(launch_bytes(tl.K_STEP, [p] * B) for p in range(P)) / P
-
-    def profile(into):
-        dec.set(tl.OPT_PROFILE, 1)
-        dec.prof_reset()
-        dec.greedy(tok0, pos0, P, want_tokens=False, sync=True)
-        for k, name in enumerate(tl.K_NAMES):
-            ms, n = dec.prof(k)
-            if n:
-                into[name] = {"avg_us": 1e3 * ms / n, "launches": n}
-                if k == tl.K_STEP:
-                    into[name]["GBps"] = step_bytes_p / (into[name]["avg_us"] * 1e-6) / 1e9
-                elif k not in (tl.K_ATTN, tl.K_ARGMAX):
-                    into[name]["GBps"] = launch_bytes(k, [0] * B) / (into[name]["avg_us"] * 1e-6) / 1e9
-        dec.set(tl.OPT_PROFILE, 0)
-
-    if rank == 0:
-        profile(prof)
+        def run(into):
+            dec.set(tl.OPT_PROFILE, 1)
+            dec.prof_reset()
+            dec.greedy([1] * B, [0] * B, P, want_tokens=False, sync=True)
+            for k, name in enumerate(tl.K_NAMES):
+                ms, n = dec.prof(k)
+                if n:
+                    into[name] = {"avg_us": 1e3 * ms / n, "launches": n}
+                    if k == tl.K_STEP:
+                        into[name]["GBps"] = step_bytes_p / (into[name]["avg_us"] * 1e-6) / 1e9
+                    elif k not in (tl.K_ATTN, tl.K_ARGMAX):
+                        into[name]["GBps"] = launch_bytes(B, k, [0] * B) / (into[name]["avg_us"] * 1e-6) / 1e9
+            dec.set(tl.OPT_PROFILE, 0)
+        run(prof)
         if persistent:
             dec.set(tl.OPT_PERSISTENT, 0)
-            profile(prof_ml)
+            run(prof_ml)
             dec.set(tl.OPT_PERSISTENT, 1)
-
-    # ---------------- CPU baseline: the oracle (bit-exact seq.cpp / runq.c restatement), same model,
-    # on this box's host cores (BASELINE.md CPU-baseline plan): (i) one decoder on one core, like
-    # seq.cpp (int8: runq's OpenMP matmul over the cores we may use); (ii) aggregate: P
-    # independent single-threaded decoders at once, one per core, over disjoint sequences
-    cpu = None
-    if rank == 0 and world == 1 and not args.skip_cpu and args.cpu_baseline_tokens >= 0:
-        sys.path.insert(0, os.path.join(REPO, "oracle"))
-        import oracle as O
-        nproc = os.cpu_count() or 1
-        allowed = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(nproc))
-        # the GPU box grants a CPU share per GPU (OMP_NUM_THREADS there); the whole host's nproc
-        # is reported beside it
-        share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(allowed)
-        P = max(1, min(share, len(allowed), args.cpu_aggregate))
-        O.set_threads(P)  # weight synthesis (+ int8 quantisation) only
-        ref = O.Model(cfg_t, shared, seed=SEED)
-        if q8:
-            ref.build_q8(gs)
-            cores = P  # runq.c's matmul is OpenMP-parallel (runq.c:323-324)
-            run = lambda m: ref.q8_greedy(1, 0, m)
-        else:
-            O.set_threads(1)
-            cores = 1  # seq.cpp is single-threaded
-            run = lambda m: ref.greedy(1, 0, m)
-        n = args.cpu_baseline_tokens
-        t1 = None
-        if n <= 0:  # bounded sample: as many tokens as fit the time budget (one token calibrates), >= 8
-            tc = time.perf_counter()
-            run(1)
-            t1 = time.perf_counter() - tc
-            ref.reset_kv()
-            n = max(8, min(K, S, int(args.cpu_baseline_seconds / max(t1, 1e-6))))
-        tc = time.perf_counter()
-        ctoks = run(n)
-        tcpu = time.perf_counter() - tc
-        t1 = t1 or tcpu / n
-        gtoks = dec.greedy([1] * B, pos0, n)[:, 0].tolist()
-        agg = None
-        if not q8 and P > 1:
-            m_agg = max(1, min(8, int(args.cpu_baseline_seconds / max(t1, 1e-6) / 2)))
-            secs, atoks = ref.aggregate(P, m_agg, allowed[:P])
-            agg = {"value": round(P * m_agg / secs, 4), "unit": "tok/s", "cores": P, "decoders": P,
-                   "sample": f"{P} single-threaded decoders at once (one per core, pinned), decoder i greedy "
-                             f"from token 1+i at pos 0, {m_agg} token(s) each",
-                   "seconds": round(secs, 2), "decoder0_matches_single": atoks[0].tolist() == ctoks[:m_agg]}
-        cpu = {"value": round(n / tcpu, 4), "unit": "tok/s", "cores": cores, "kind": "port",
-               "sample": f"{n} greedy tokens (as many as fit ~{args.cpu_baseline_seconds:g} s, at least 8, unless "
-                         f"--cpu-baseline-tokens) from BOS (pos 0..{n - 1}) of the same synthetic {mname} "
-                         f"{args.dtype} model with oracle/oracle.c (bit-exact "
-                         f"{'runq.c' if q8 else 'src/seq.cpp'} restatement), {cores} thread(s)",
-               "host": {"nproc": nproc, "affinity_cpus": len(allowed), "cpu_share": share},
-               "aggregate": agg,
-               "tokens_match_gpu": ctoks == gtoks,
-               "tokens_match_prefix": next((i for i, (a, b) in enumerate(zip(ctoks, gtoks)) if a != b),
-                                           min(len(ctoks), len(gtoks)))}
-        ref.close()
-
-    if rank == 0:
-        roof = None
-        stp, ffn = prof.get("step"), prof.get("ffn_up")
         # HBM traffic of the same kernel from the committed rocprofv3 PMC passes (FETCH_SIZE and
-        # WRITE_SIZE in separate runs, gfx950 FETCH_SIZE x2 correction): profiles/r02_pmc_traffic*.json
-        pmc_file = "r02_pmc_traffic_int8.json" if q8 else "r02_pmc_traffic.json"
+        # WRITE_SIZE in separate runs, gfx950 FETCH_SIZE x2 correction): profiles/*pmc_traffic*.json
         pmc = {}
-        try:
-            with open(os.path.join(REPO, "profiles", pmc_file)) as f:
-                pmc = json.load(f)["kernels"]
-        except (OSError, ValueError, KeyError):
-            pmc = {}
+        for fn in (f"r03_pmc_traffic_{args.dtype}_b{B}.json", "r02_pmc_traffic_int8.json" if q8 else
+                   "r02_pmc_traffic.json"):
+            try:
+                with open(os.path.join(REPO, "profiles", fn)) as f:
+                    j = json.load(f)
+                if j.get("model", mname) == mname and j.get("batch", 1) == B:
+                    pmc = {"file": fn, "kernels": j["kernels"]}
+                    break
+            except (OSError, ValueError, KeyError):
+                continue
 
         def traffic_of(prefix):
-            if mname != "llama2-7B" or B != 1:
-                return None  # the committed PMC passes were taken on the 7B batch-1 workloads
-            hits = [v["traffic_bytes"] for k, v in pmc.items() if k.startswith(prefix)]
-            return round(hits[0]) if hits else None
+            hits = [v["traffic_bytes"] for k, v in pmc.get("kernels", {}).items() if k.startswith(prefix)]
+            return round(hits[0]) if hits and mname == "llama2-7B" else None
+        stp, ffn = prof.get("step"), prof.get("ffn_up")
+        roof = None
         if stp:
             roof = {"bound": "hbm", "achieved": round(stp["GBps"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(stp["GBps"] / HBM_PEAK_GBS, 4),
-                    "traffic": traffic_of("void tl::persistent_step_kernel<"),
-                    "traffic_source": f"profiles/{pmc_file} (rocprofv3 --pmc, mean over the run's launches: "
-                                      "positions 0..255, so ~0.1 GB more K/V than positions 0..15)",
-                    "kernel": "persistent_step_kernel (the whole decode step, one launch)",
+                    "traffic": traffic_of("void tl::persistent_step_kernel<") if pmc else None,
+                    "traffic_source": f"profiles/{pmc['file']} (rocprofv3 --pmc)" if pmc else None,
+                    "kernel": f"persistent_step_kernel (the whole decode step of {B} sequence(s), one launch)",
                     "bytes_per_launch": step_bytes_p, "avg_us": round(stp["avg_us"], 2),
                     "positions": f"0..{P - 1}"}
         elif ffn:
+            mfma = B >= 4
+            kname = ("gemv_q8" if q8 else "gemv") + ("_mfma" if mfma else "") + "_kernel"
             roof = {"bound": "hbm", "achieved": round(ffn["GBps"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ffn["GBps"] / HBM_PEAK_GBS, 4),
-                    "traffic": None if q8 else traffic_of("void tl::gemv_kernel<2, 1, 1, true, 4, false>"),
-                    "traffic_source": f"profiles/{pmc_file} (rocprofv3 --pmc)",
-                    "kernel": ("gemv_q8" if q8 else "gemv") + ("_mfma" if B >= 4 else "") + "_kernel<GM_SWIGLU> "
-                              "(RMSNorm + W1/W3 + SwiGLU" + (", matrix cores)" if B >= 4 else ")"),
-                    "bytes_per_launch": launch_bytes(tl.K_FFN_UP, [0] * B), "avg_us": round(ffn["avg_us"], 2)}
-        out = {
-            "metric": "decode tokens/sec (greedy, whole model) + achieved HBM GB/s fraction",
-            "value": round(value, 3), "unit": "tok/s", "n_gpus": world, "steps": K, "warmup": W,
-            "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": args.dtype, "data": "synthetic (random-init weights, BOS-started greedy decode)",
-            "config": {"workload": f"{mname} {args.dtype} greedy decode, {B} seq/GPU, positions 0..{K - 1}",
-                       "model": mname, "global_batch": B * world, "seq_len": S, "parallelism": f"prompt-dp{world}"},
-            "hbm": {"step_bytes": step_bytes, "achieved_GBps": round(step_gbs, 1),
-                    "frac_of_peak": round(step_gbs / HBM_PEAK_GBS, 4),
-                    "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / step_bytes * B * world, 1)},
-            "roofline": roof,
-            "step_path": "persistent" if persistent_after else "multi-launch",
-            "persistent_fallback": bool(persistent and not persistent_after),
-            "persistent_launch": (("cooperative" if tl.lib().thallama_persistent_cooperative() else "plain")
-                                  if persistent else None),
-            "headline": headline,
-            "reference_tokens": golden,
-            "kernels": {k: {kk: round(vv, 2) for kk, vv in v.items()} for k, v in prof.items()},
-            "kernels_multilaunch": {k: {kk: round(vv, 2) for kk, vv in v.items()} for k, v in prof_ml.items()},
-            "cpu_baseline": cpu,
-            "init_s": round(t_init, 2), "broadcast_s": round(t_bcast, 2),
-        }
+                    "traffic": traffic_of(f"void tl::{kname}<2") if pmc else None,
+                    "traffic_source": f"profiles/{pmc['file']} (rocprofv3 --pmc)" if pmc else None,
+                    "kernel": f"{kname}<GM_SWIGLU> (RMSNorm + W1/W3 + SwiGLU)",
+                    "bytes_per_launch": launch_bytes(B, tl.K_FFN_UP, [0] * B), "avg_us": round(ffn["avg_us"], 2)}
+        rnd = lambda d: {k: {kk: round(vv, 2) for kk, vv in v.items()} for k, v in d.items()}  # noqa: E731
+        return roof, rnd(prof), rnd(prof_ml)
+
+    # ------------------------------------------------------------ request workload (configs[4])
+    def requests_run(dec, B, n_per_rank, passes, warm, fixture_write=False):
+        """The reference test mode over gen_in_64.txt: n_per_rank prompts per rank, B slots, greedy,
+        each request to position T-1 or EOS/BOS.  Returns the measurement dict (rank 0)."""
+        from hip_llama_cpp_amd import host as H
+        n = n_per_rank * world
+        wd = tempfile.mkdtemp(prefix=".bench_", dir=REPO) if rank == 0 else None
+        prompts = read_prompts(PROMPTS, n)
+        req = write_requests(prompts, wd) if rank == 0 else None
+        if world > 1:
+            box = [req, wd]
+            dist.broadcast_object_list(box, src=0)
+            req, wd = box
+        out = os.path.join(wd, "out.txt")
+        tok = H.Tokenizer(TOKENIZER)
+        prompt_pos = sum(max(0, min(len(tok.encode(p)), T) - 1) for p in prompts)  # prefilled / forced positions
+        mtl = tok.max_token_length
+        tok.close()
+        native = (tl.C.cast(tl.lib().thallama_decoder_step_cb, tl.C.c_void_p).value,
+                  tl.C.cast(tl.lib().thallama_decoder_prefill_cb, tl.C.c_void_p).value, dec.h.value)
+        gen, outs = [0], []
+
+        def one():
+            outs.clear()
+            gen[0] = D.serve_sharded(req, out, TOKENIZER, abs(c.vocab_size), B, None, mtl, T, temperature=0.0,
+                                     workdir=wd, native=native, outputs=outs)
+        for _ in range(warm):
+            one()
+        el = timed(one, passes)
+        res = None
+        if rank == 0:
+            outs = [o.decode("utf-8", "replace") for o in outs]
+            fx_path = os.path.join(GOLDEN, f"bench_requests_{mname}_{args.dtype}_greedy.json")
+            match, fx_n = None, 0
+            if fixture_write:
+                with open(fx_path, "w") as f:
+                    json.dump({"generator": "bench.py --write-fixture (one process, one GPU, "
+                                            f"{B} slots over all {n} prompts)",
+                               "model": mname, "dtype": args.dtype, "seed": SEED, "decode_len": T,
+                               "prompts": "tests/golden/gen_in_64.txt (reference assets/in/gen_in_64.txt)",
+                               "outputs": outs}, f, indent=0)
+            if os.path.exists(fx_path):
+                with open(fx_path) as f:
+                    fx = json.load(f)
+                if fx.get("decode_len") == T and fx.get("seed") == SEED:
+                    fx_n = min(len(outs), len(fx["outputs"]))
+                    match = outs[:fx_n] == fx["outputs"][:fx_n]
+            tok_s = gen[0] * passes / el
+            dec_tokens = gen[0] - prompt_pos
+            per_rank_roof = HBM_PEAK_GBS * 1e9 / token_bytes(B, (T - 1) / 2.0) * B
+            res = {"workload": f"{mname} {args.dtype} test mode (src/llama.cpp:891-1083), greedy, {n} prompts of "
+                               f"gen_in_64.txt ({n_per_rank} per GPU, {B} slots per GPU, prompt prefilled), each "
+                               f"request to position {T - 1} or EOS/BOS",
+                   "value": round(tok_s, 3), "unit": "tok/s", "seconds_per_pass": round(el / passes, 4),
+                   "passes": passes, "tokens_per_pass": gen[0],
+                   "decode_tok_s": round(dec_tokens * passes / el, 3),
+                   "prompt_positions_per_pass": prompt_pos,
+                   "roofline_decode_tok_s_per_gpu": round(per_rank_roof, 1),
+                   "frac_of_roofline": round(dec_tokens * passes / el / world / per_rank_roof, 4),
+                   "outputs_sha": sha(outs), "output_matches_fixture": match, "fixture_requests_compared": fx_n,
+                   "fixture": os.path.relpath(fx_path, REPO) if os.path.exists(fx_path) else None}
+            os.remove(out)
+            os.remove(req)
+            os.rmdir(wd)
+        if world > 1:
+            dist.barrier()
+        return res
+
+    out = None
+    if workload == "requests":
+        B = args.batch or 8
+        state, dec = make_decoder(B)
+        log(f"[rank {rank}] {mname} {args.dtype} requests B={B} init {t_init:.2f}s (broadcast {t_bcast:.2f}s) "
+            f"path {'persistent' if dec.persistent() else 'multi-launch'}")
+        per = 64 if args.write_fixture else args.prompts_per_gpu
+        if per * world > 64:
+            raise SystemExit(f"{per} prompts per GPU x {world} GPUs > the 64 prompts of gen_in_64.txt")
+        r = requests_run(dec, B, per, args.steps, args.warmup, fixture_write=args.write_fixture and world == 1)
+        roof, prof, prof_ml = profile_roofline(dec, B) if rank == 0 else (None, {}, {})
+        if rank == 0:
+            out = {"metric": "decode tokens/sec (greedy, whole model) + achieved HBM GB/s fraction",
+                   "value": r["value"], "unit": "tok/s", "n_gpus": world, "steps": args.steps,
+                   "warmup": args.warmup, "ms_per_step": round(1e3 * r["seconds_per_pass"], 3),
+                   "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+                   "data": "synthetic weights (random init, seed 20240224); prompts: the reference's gen_in_64.txt",
+                   "config": {"workload": r["workload"], "model": mname, "global_batch": per * world,
+                              "slots_per_gpu": B, "seq_len": S, "decode_len": T, "parallelism": f"prompt-dp{world}"},
+                   "requests": r, "roofline": roof, "kernels": prof, "kernels_multilaunch": prof_ml,
+                   "cpu_baseline": None, "init_s": round(t_init, 2), "broadcast_s": round(t_bcast, 2)}
+    else:
+        B = args.batch or 1
+        state, dec = make_decoder(B)
+        persistent = dec.persistent()
+        log(f"[rank {rank}] {mname} {args.dtype} B={B} init {t_init:.2f}s (broadcast {t_bcast:.2f}s) "
+            f"path {'persistent' if persistent else 'multi-launch'}")
+        tok0, pos0 = [1] * B, [0] * B  # BOS at position 0
+
+        def decode():
+            dec.greedy(tok0, pos0, T, want_tokens=False, sync=False)
+        for _ in range(args.warmup):
+            decode()
+        elapsed = timed(decode, args.steps)
+        dec.sync()
+        K = args.steps
+        value = world * B * T * K / elapsed
+        ms_step = elapsed / K * 1e3
+        persistent_after = dec.persistent()
+        step_bytes = sum(token_bytes(B, p) for p in range(T)) / T  # per token step, mean over positions
+        step_gbs = step_bytes * T * K / elapsed / 1e9
+
+        # greedy tokens vs the reference's own 256-step decode (tests/golden/reference_long.json,
+        # generated from the reference's seq.cpp / runq.c by make_golden_long.py)
+        golden = None
+        try:
+            with open(os.path.join(GOLDEN, "reference_long.json")) as f:
+                gcases = json.load(f)["cases"]
+        except (OSError, ValueError, KeyError):
+            gcases = []
+        for gc in gcases:
+            if tuple(gc["config"]) == tuple(cfg_t) and gc["shared"] == shared and gc["seed"] == SEED:
+                want = gc["q8" if q8 else "fp32"]["tokens"]
+                got = dec.greedy(tok0, pos0, len(want))  # [steps][B]
+                prefix = min(next((i for i, (a, b) in enumerate(zip(want, got[:, b].tolist())) if a != b), len(want))
+                             for b in range(B))
+                golden = {"steps": len(want), "tokens_match": prefix == len(want), "match_prefix": prefix,
+                          "source": "tests/golden/reference_long.json (" + ("runq.c" if q8 else "src/seq.cpp") +
+                                    " compiled from the reference, greedy from BOS)"}
+
+        # long context: positions 1792..2047 of a 2048-token decode (the reference's test mode runs
+        # every request to seq_len, src/llama.cpp:1584), tokens against tests/golden/reference_2048.json
+        long_ctx = None
+        if not args.no_long and S >= 2048 and rank == 0:
+            t_tail = 256
+            toks_all = dec.greedy(tok0, pos0, S)  # the whole decode (untimed), tokens for the comparison
+            # replay its last t_tail positions: every K/V row before them is in place; the input at
+            # position S - t_tail is the token generated at the position before
+            last_tok = [int(v) for v in toks_all[S - t_tail - 1]]
+            torch.cuda.synchronize()
+            tc = time.perf_counter()
+            dec.greedy(last_tok, [S - t_tail] * B, t_tail, want_tokens=False, sync=True)
+            lt = time.perf_counter() - tc
+            tail_bytes = sum(token_bytes(B, p) for p in range(S - t_tail, S)) / t_tail
+            long_ctx = {"workload": f"positions {S - t_tail}..{S - 1} of a {S}-token greedy decode from BOS "
+                                    f"({B} seq/GPU)",
+                        "value": round(B * t_tail / lt, 3), "unit": "tok/s", "ms_per_token": round(lt / t_tail * 1e3, 4),
+                        "achieved_GBps": round(tail_bytes * t_tail / lt / 1e9, 1),
+                        "frac_of_peak": round(tail_bytes * t_tail / lt / 1e9 / HBM_PEAK_GBS, 4),
+                        "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / tail_bytes * B, 1)}
+            try:
+                with open(os.path.join(GOLDEN, "reference_2048.json")) as f:
+                    g2 = json.load(f)
+                if not q8 and tuple(g2["config"]) == tuple(cfg_t) and g2["seed"] == SEED:
+                    want = g2["tokens"]
+                    pre = min(next((i for i, (a, b) in enumerate(zip(want, toks_all[:, b].tolist())) if a != b),
+                                   len(want)) for b in range(B))
+                    long_ctx["reference_tokens"] = {"steps": len(want), "match_prefix": pre,
+                                                    "tokens_match": pre == len(want),
+                                                    "source": "tests/golden/reference_2048.json"}
+            except (OSError, ValueError, KeyError):
+                pass
+
+        roof, prof, prof_ml = profile_roofline(dec, B) if rank == 0 else (None, {}, {})
+
+        # the 1-GPU point of the request workload (configs[4]'s per-GPU share), so the N > 1 lines
+        # have their own single-GPU reference
+        req_point = None
+        if world == 1 and not args.no_requests_point and not q8 and mname == "llama2-7B":
+            del dec, state
+            torch.cuda.empty_cache()
+            st8, dec8 = make_decoder(8)
+            req_point = requests_run(dec8, 8, args.prompts_per_gpu, 1, 1)
+            del dec8, st8
+            state, dec = make_decoder(B)  # (the CPU baseline compares against a fresh decoder)
+
+        # CPU baseline: the oracle (bit-exact seq.cpp / runq.c restatement), same model, on this box's
+        # host cores: (i) one decoder on one core, like seq.cpp (int8: runq's OpenMP matmul over the
+        # cores we may use); (ii) aggregate: P single-threaded decoders at once, one per core
+        cpu = None
+        if rank == 0 and world == 1 and not args.skip_cpu and args.cpu_baseline_tokens >= 0:
+            sys.path.insert(0, os.path.join(REPO, "oracle"))
+            import oracle as O
+            nproc = os.cpu_count() or 1
+            allowed = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(nproc))
+            # the GPU box grants a CPU share per GPU (OMP_NUM_THREADS there); the whole host's nproc
+            # is reported beside it
+            share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(allowed)
+            P = max(1, min(share, len(allowed), args.cpu_aggregate))
+            O.set_threads(P)  # weight synthesis (+ int8 quantisation) only
+            ref = O.Model(cfg_t, shared, seed=SEED)
+            if q8:
+                ref.build_q8(gs)
+                cores = P  # runq.c's matmul is OpenMP-parallel (runq.c:323-324)
+                run = lambda m: ref.q8_greedy(1, 0, m)  # noqa: E731
+            else:
+                O.set_threads(1)
+                cores = 1  # seq.cpp is single-threaded
+                run = lambda m: ref.greedy(1, 0, m)  # noqa: E731
+            n = args.cpu_baseline_tokens
+            t1 = None
+            if n <= 0:  # bounded sample: as many tokens as fit the time budget (one token calibrates), >= 8
+                tc = time.perf_counter()
+                run(1)
+                t1 = time.perf_counter() - tc
+                ref.reset_kv()
+                n = max(8, min(T, S, int(args.cpu_baseline_seconds / max(t1, 1e-6))))
+            tc = time.perf_counter()
+            ctoks = run(n)
+            tcpu = time.perf_counter() - tc
+            t1 = t1 or tcpu / n
+            gtoks = dec.greedy([1] * B, pos0, n)[:, 0].tolist()
+            agg = None
+            if not q8 and P > 1:
+                m_agg = max(1, min(8, int(args.cpu_baseline_seconds / max(t1, 1e-6) / 2)))
+                secs, atoks = ref.aggregate(P, m_agg, allowed[:P])
+                agg = {"value": round(P * m_agg / secs, 4), "unit": "tok/s", "cores": P, "decoders": P,
+                       "sample": f"{P} single-threaded decoders at once (one per core, pinned), decoder i greedy "
+                                 f"from token 1+i at pos 0, {m_agg} token(s) each",
+                       "seconds": round(secs, 2), "decoder0_matches_single": atoks[0].tolist() == ctoks[:m_agg]}
+            cpu = {"value": round(n / tcpu, 4), "unit": "tok/s", "cores": cores, "kind": "port",
+                   "sample": f"{n} greedy tokens (as many as fit ~{args.cpu_baseline_seconds:g} s, at least 8, unless "
+                             f"--cpu-baseline-tokens) from BOS (pos 0..{n - 1}) of the same synthetic {mname} "
+                             f"{args.dtype} model with oracle/oracle.c (bit-exact "
+                             f"{'runq.c' if q8 else 'src/seq.cpp'} restatement), {cores} thread(s)",
+                   "host": {"nproc": nproc, "affinity_cpus": len(allowed), "cpu_share": share},
+                   "aggregate": agg,
+                   "tokens_match_gpu": ctoks == gtoks,
+                   "tokens_match_prefix": next((i for i, (a, b) in enumerate(zip(ctoks, gtoks)) if a != b),
+                                               min(len(ctoks), len(gtoks)))}
+            ref.close()
+
+        if rank == 0:
+            out = {
+                "metric": "decode tokens/sec (greedy, whole model) + achieved HBM GB/s fraction",
+                "value": round(value, 3), "unit": "tok/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
+                "ms_per_step": round(ms_step, 3), "ms_per_token": round(ms_step / T, 4), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+                "data": "synthetic (random-init weights, BOS-started greedy decode)",
+                "config": {"workload": f"{mname} {args.dtype} {T}-token greedy decode from BOS (positions 0..{T - 1}), "
+                                       f"{B} seq/GPU; one step = one whole decode",
+                           "model": mname, "global_batch": B * world, "seq_len": S, "decode_len": T,
+                           "parallelism": f"prompt-dp{world}"},
+                "hbm": {"step_bytes": step_bytes, "achieved_GBps": round(step_gbs, 1),
+                        "frac_of_peak": round(step_gbs / HBM_PEAK_GBS, 4),
+                        "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / step_bytes * B * world, 1)},
+                "roofline": roof,
+                "step_path": "persistent" if persistent_after else "multi-launch",
+                "persistent_fallback": bool(persistent and not persistent_after),
+                "persistent_launch": (("cooperative" if tl.lib().thallama_persistent_cooperative() else "plain")
+                                      if persistent else None),
+                "reference_tokens": golden,
+                "long_context": long_ctx,
+                "requests_1gpu": req_point,
+                "kernels": prof, "kernels_multilaunch": prof_ml,
+                "cpu_baseline": cpu,
+                "init_s": round(t_init, 2), "broadcast_s": round(t_bcast, 2),
+            }
+    if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -126,6 +126,7 @@ struct thallama_decoder {
   float* xn_d = nullptr;        // [<=16][dim] normed rows for the matrix-core GEMV (batch >= 2)
   float* ssq_d = nullptr;       // [B][dim/16] per-tile sums of squares carried from Wo / W2 to the next norm
   bool no_ssq = false;          // THALLAMA_NO_SSQ=1: the norm prologue launch instead (A/B measurement)
+  bool ssq_carry = false;       // this step carries them (ssq_carry_ok)
   signed char* xq_d = nullptr;  // int8 batched: activations quantised once per launch [8][max(dim, hidden)]
   float* xqs_d = nullptr;       //   and their group scales
   signed char* hq_d = nullptr;  // int8 4..8 sequences: SwiGLU output quantised for W2 [8][hidden]
@@ -144,7 +145,8 @@ struct thallama_decoder {
   bool persist = true;          // requested (THALLAMA_OPT_PERSISTENT)
   bool pfault = false;          // test hook: the next persistent launch loses block 0
   bool pasync = false;          // an asynchronous greedy call ran persistent launches not yet checked
-  hipGraphExec_t exec = nullptr;
+  hipGraphExec_t exec = nullptr;      // one greedy step (step + argmax), replayed per token
+  hipGraphExec_t exec_fwd = nullptr;  // one forward step (no argmax), replayed by decoder_forward
   // persistent one-launch step (persist.hip)
   int ncu = 0;
   unsigned* psync = nullptr;    // [kPSyncWords shards][L*H tickets] (zeroed per launch), err, seq
@@ -169,6 +171,14 @@ struct thallama_decoder {
   double prof_ms[THALLAMA_K_COUNT] = {0};
   long long prof_n[THALLAMA_K_COUNT] = {0};
 };
+
+// Options, buffers and the persistent path's state are baked into the captured graphs: drop them
+// (recaptured on next use).
+static void drop_graphs(thallama_decoder* d) {
+  if (d->exec) (void)hipGraphExecDestroy(d->exec);
+  if (d->exec_fwd) (void)hipGraphExecDestroy(d->exec_fwd);
+  d->exec = d->exec_fwd = nullptr;
+}
 
 static int prof_begin(thallama_decoder* d) {
   if (!d->profile) return -1;
@@ -285,6 +295,7 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
     const size_t nblk = (size_t)tl::mfma_target_blocks();
     TL_TRY(hipMalloc(&d->xn_d, sizeof(float) * (size_t)(batch < 16 ? batch : 16) * d->dim));
     TL_TRY(hipMalloc(&d->ssq_d, sizeof(float) * (size_t)batch * ((d->dim + 15) / 16)));
+    TL_TRY(hipMemset(d->ssq_d, 0, sizeof(float) * (size_t)batch * ((d->dim + 15) / 16)));
     const char* e = getenv("THALLAMA_NO_SSQ");
     d->no_ssq = e && e[0] == '1';
     TL_TRY(hipMalloc(&d->mpart_d, sizeof(float) * nblk * 2 * 256));
@@ -330,7 +341,7 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
 extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   if (!d) return;
   (void)hipStreamSynchronize(d->stream);
-  if (d->exec) (void)hipGraphExecDestroy(d->exec);
+  drop_graphs(d);
   for (auto e : d->ev_pool) (void)hipEventDestroy(e);
   (void)hipFree(d->tok_d);
   (void)hipFree(d->pos_d);
@@ -370,14 +381,11 @@ extern "C" int thallama_decoder_set(thallama_decoder* d, int key, int value) {
     case THALLAMA_OPT_PERSISTENT: d->persist = value != 0; break;
     case THALLAMA_OPT_PERSIST_FAULT:
       d->pfault = value != 0;
-      if (d->exec) { (void)hipGraphExecDestroy(d->exec); d->exec = nullptr; }
+      drop_graphs(d);
       break;
     default: return (int)hipErrorInvalidValue;
   }
-  if (d->exec) {  // options are baked into a captured graph: recapture on next use
-    (void)hipGraphExecDestroy(d->exec);
-    d->exec = nullptr;
-  }
+  drop_graphs(d);  // options are baked into a captured graph: recapture on next use
   return 0;
 }
 
@@ -431,13 +439,30 @@ static int q8_ffn_quant(const thallama_decoder* d) {
 // fp32 batched steps on the matrix cores: the residual launches (Wo, W2) leave per-tile sums of
 // squares of the residual stream and the next normed launch reduces them instead of running a
 // norm prologue launch (gemv_mfma.hpp).  Both ends use the matrix-core kernel or neither (same nb).
+// The sums are carried only when EVERY residual launch of the step takes one of the two kernels
+// that write them (gemv_matrix_path, the launcher's own predicate): W2 has K = hidden, which can
+// fail the matrix-path shape while K = dim passes (e.g. dim 512, hidden 1376), and a consumer
+// would then read sums the previous step or another layer left.  Consumers that do not take the
+// matrix path ignore ssq_in (the streaming kernels normalise from x).
+static bool ssq_carry_ok(const thallama_decoder* d) {
+  if (d->q8 || !d->ssq_d || d->no_ssq || (d->dim + 15) / 16 > 256) return false;  // (the kernel sums <= 256 tiles)
+  for (int l = 0; l < d->L; ++l) {
+    tl::GemvParams wo = {}, w2 = {};
+    wo.W0 = d->w.wo + (long long)l * d->dim * d->dim;
+    wo.K = d->dim; wo.n_items = d->dim; wo.nb = d->B; wo.x = d->s.xb; wo.x_stride = d->dim;
+    w2.W0 = d->w.w2 + (long long)l * d->dim * d->hidden;
+    w2.K = d->hidden; w2.n_items = d->dim; w2.nb = d->B; w2.x = d->s.hb; w2.x_stride = d->hidden;
+    if (!tl::gemv_matrix_path(wo) || !tl::gemv_matrix_path(w2)) return false;
+  }
+  return true;
+}
 static void ssq_to_next_norm(const thallama_decoder* d, tl::GemvParams& p) {
-  if (d->q8 || !d->ssq_d) return;
+  if (!d->ssq_carry) return;
   p.ssq_out = d->ssq_d;
   p.ssq_nt = (d->dim + 15) / 16;
 }
 static void norm_from_ssq(const thallama_decoder* d, tl::GemvParams& p) {
-  if (d->q8 || !d->ssq_d || d->no_ssq || (d->dim + 15) / 16 > 256) return;  // (the kernel sums <= 256 tiles)
+  if (!d->ssq_carry) return;
   p.ssq_in = d->ssq_d;
   p.ssq_nt = (d->dim + 15) / 16;
 }
@@ -447,6 +472,7 @@ static int enqueue_step(thallama_decoder* d) {
   const long long kv_b_stride = (long long)d->L * S * kvd;
   const TransformerWeights& w = d->w;
   const RunState& s = d->s;
+  d->ssq_carry = ssq_carry_ok(d);
   for (int l = 0; l < d->L; ++l) {
     const long long ll = l;
     // 1. QKV (+ embedding at layer 0)
@@ -696,10 +722,7 @@ static int check_persist(thallama_decoder* d) {
   TL_TRY(hipMemset(d->cnt_d, 0, sizeof(unsigned) * (size_t)d->B * d->H));
   d->pok = false;
   d->pwhy = "a grid barrier timed out";
-  if (d->exec) {  // the captured graph holds the persistent launch
-    (void)hipGraphExecDestroy(d->exec);
-    d->exec = nullptr;
-  }
+  drop_graphs(d);  // the captured graphs hold the persistent launch
   g_last_error = "persistent step: a grid barrier timed out (grid not co-resident); path disabled";
   return kPersistFellBack;
 }
@@ -727,7 +750,7 @@ extern "C" int thallama_decoder_ptrace(thallama_decoder* d, int enable, unsigned
     TL_TRY(hipMalloc(&d->ptrace, need * sizeof(unsigned long long)));
     TL_TRY(hipMemset(d->ptrace, 0, need * sizeof(unsigned long long)));
     d->ptrace_n = need;
-    if (d->exec) { (void)hipGraphExecDestroy(d->exec); d->exec = nullptr; }
+    drop_graphs(d);
   }
   if (host && d->ptrace) {
     TL_TRY(hipStreamSynchronize(d->stream));
@@ -793,8 +816,22 @@ static int decoder_forward_once(thallama_decoder* d, const int* token_h, const i
   if (!d || !token_h || !pos_h) return (int)hipErrorInvalidValue;
   int r = upload_tok_pos(d, token_h, pos_h);
   if (r) return r;
-  r = use_persist(d) ? enqueue_persistent(d, false) : enqueue_step(d);
-  if (r) return r;
+  if (d->use_graph && !d->profile) {  // the step (~160 launches at batch > 1) replayed as one graph
+    if (!d->exec_fwd) {
+      hipGraph_t g = nullptr;
+      TL_TRY(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
+      const int e = use_persist(d) ? enqueue_persistent(d, false) : enqueue_step(d);
+      hipError_t ce = hipStreamEndCapture(d->stream, &g);
+      if (e) return e;
+      TL_TRY(ce);
+      TL_TRY(hipGraphInstantiate(&d->exec_fwd, g, nullptr, nullptr, 0));
+      (void)hipGraphDestroy(g);
+    }
+    TL_TRY(hipGraphLaunch(d->exec_fwd, d->stream));
+  } else {
+    r = use_persist(d) ? enqueue_persistent(d, false) : enqueue_step(d);
+    if (r) return r;
+  }
   if (logits_h)
     TL_TRY(hipMemcpyAsync(logits_h, d->s.logits, sizeof(float) * (size_t)d->B * d->V, hipMemcpyDeviceToHost,
                           d->stream));
@@ -873,6 +910,23 @@ static int decoder_greedy_once(thallama_decoder* d, const int* token0_h, const i
   return check_persist(d);
 }
 
+// thallama_step_fn / thallama_prefill_fn (include/thallama_host.h) over one decoder (ctx), so a
+// host scheduler can drive it with no glue of its own (bench.py's request workload).
+extern "C" int thallama_decoder_step_cb(void* ctx, int worker, int batch, const int* token, const int* pos,
+                                        float* logits) {
+  (void)worker;
+  thallama_decoder* d = (thallama_decoder*)ctx;
+  if (!d || batch != d->B) return (int)hipErrorInvalidValue;
+  return thallama_decoder_forward(d, token, pos, logits);
+}
+
+extern "C" int thallama_decoder_prefill_cb(void* ctx, int worker, int slot, const int* tokens, int n, int pos0) {
+  (void)worker;
+  const int st = thallama_decoder_prefill((thallama_decoder*)ctx, slot, tokens, n, pos0);
+  if (st == (int)hipErrorNotSupported) return 1;  // the scheduler then steps through the prompt
+  return st ? -st : 0;
+}
+
 extern "C" int thallama_decoder_logits(thallama_decoder* d, float* logits_h) {
   if (!d || !logits_h) return (int)hipErrorInvalidValue;
   TL_TRY(hipMemcpyAsync(logits_h, d->s.logits, sizeof(float) * (size_t)d->B * d->V, hipMemcpyDeviceToHost,
@@ -931,16 +985,75 @@ extern "C" double thallama_step_bytes(const Config* c, int B, int kclass, const 
 }
 
 // ------------------------------------------------------------------ thaDNN_s_forward_batch
-// The reference signature carries no workspace, so one decoder per
-// (device, stream, weights, state, batch, config) is created on first use and reused.
+// The reference signature carries no workspace, so a decoder per (device, stream, batch, config,
+// fp32|int8) is created on first use and reused.  A call with other weight / state buffers than
+// the cached decoder's replaces it (the old one and its workspace are freed), and at most
+// kDecCacheMax decoders live at once (least recently used evicted), so a host that reallocates
+// its buffers does not grow without bound.  thallama_forward_batch_cache_size() reports the count.
 namespace {
-typedef std::tuple<int, hipStream_t, const void*, const void*, const void*, int, int, int, int, int> DecKey;
+typedef std::tuple<int, hipStream_t, int, int, int, int, int, int, int, int> DecKey;
+struct DecEntry {
+  thallama_decoder* d;
+  unsigned long long used;
+  TransformerWeights w;     // fp32 buffers the decoder was made for
+  Q8TransformerWeights w8;  // (int8)
+  RunState s;
+};
+constexpr size_t kDecCacheMax = 8;
 std::mutex g_dec_mu;
-std::map<DecKey, thallama_decoder*>& dec_cache() {
-  static std::map<DecKey, thallama_decoder*> m;
+unsigned long long g_dec_clock = 0;
+std::map<DecKey, DecEntry>& dec_cache() {
+  static std::map<DecKey, DecEntry> m;
   return m;
 }
+
+// The cached decoder for key, if it was made for exactly these buffers; else a new one (replacing
+// a stale entry, evicting the least recently used beyond the cap).  Caller holds g_dec_mu.
+thallama_decoder* dec_lookup(const DecKey& key, const Config* p, const TransformerWeights* w,
+                             const Q8TransformerWeights* w8, const RunState* s, int B, hipStream_t st) {
+  auto& m = dec_cache();
+  auto it = m.find(key);
+  if (it != m.end()) {
+    DecEntry& e = it->second;
+    const bool same = memcmp(&e.s, s, sizeof(RunState)) == 0 &&
+                      (w8 ? memcmp(&e.w8, w8, sizeof(*w8)) == 0 : memcmp(&e.w, w, sizeof(*w)) == 0);
+    if (same) {
+      e.used = ++g_dec_clock;
+      return e.d;
+    }
+    thallama_decoder_destroy(e.d);
+    m.erase(it);
+  }
+  while (m.size() >= kDecCacheMax) {
+    auto lru = m.begin();
+    for (auto i = m.begin(); i != m.end(); ++i)
+      if (i->second.used < lru->second.used) lru = i;
+    thallama_decoder_destroy(lru->second.d);
+    m.erase(lru);
+  }
+  thallama_decoder* d = nullptr;
+  const int r = w8 ? thallama_decoder_create_q8(&d, p, w8, s, B, st) : thallama_decoder_create(&d, p, w, s, B, st);
+  if (r != 0) return nullptr;
+  DecEntry e = {};
+  e.d = d;
+  e.used = ++g_dec_clock;
+  if (w8) e.w8 = *w8; else e.w = *w;
+  e.s = *s;
+  m[key] = e;
+  return d;
+}
 }  // namespace
+
+extern "C" int thallama_forward_batch_cache_size(void) {
+  std::lock_guard<std::mutex> g(g_dec_mu);
+  return (int)dec_cache().size();
+}
+
+extern "C" void thallama_forward_batch_cache_clear(void) {
+  std::lock_guard<std::mutex> g(g_dec_mu);
+  for (auto& kv : dec_cache()) thallama_decoder_destroy(kv.second.d);
+  dec_cache().clear();
+}
 
 extern "C" thablasStatus_t thaDNN_s_forward_batch(thablasHandle_t handle1, thablasHandle_t handle2,
                                                   thablasHandle_t handle3, int n_batches, Config* p,
@@ -951,22 +1064,15 @@ extern "C" thablasStatus_t thaDNN_s_forward_batch(thablasHandle_t handle1, thabl
   if (!p || !w || !s_batch || !token || !pos || !logits_host || n_batches <= 0) return THABLAS_STATUS_INVALID_VALUE;
   int dev = 0;
   CHECK_HIP(hipGetDevice(&dev));
-  DecKey key(dev, handle1.calc_stream, (const void*)w->wq, (const void*)s_batch->key_cache,
-             (const void*)s_batch->x, n_batches, p->dim, p->n_layers, p->seq_len, p->vocab_size);
+  DecKey key(dev, handle1.calc_stream, n_batches, p->dim, p->hidden_dim, p->n_layers, p->n_heads, p->n_kv_heads,
+             p->seq_len, p->vocab_size);
   thallama_decoder* d = nullptr;
   {
     std::lock_guard<std::mutex> g(g_dec_mu);
-    auto it = dec_cache().find(key);
-    if (it != dec_cache().end()) {
-      d = it->second;
-      d->w = *w;
-      d->s = *s_batch;
-    } else {
-      if (thallama_decoder_create(&d, p, w, s_batch, n_batches, handle1.calc_stream) != 0) {
-        fprintf(stderr, "thaDNN_s_forward_batch: %s\n", thallama_last_error());
-        return THABLAS_STATUS_INVALID_VALUE;
-      }
-      dec_cache()[key] = d;
+    d = dec_lookup(key, p, w, nullptr, s_batch, n_batches, handle1.calc_stream);
+    if (!d) {
+      fprintf(stderr, "thaDNN_s_forward_batch: %s\n", thallama_last_error());
+      return THABLAS_STATUS_INVALID_VALUE;
     }
   }
   // The reference's scheduler (src/llama.cpp:961-1017) runs every slot of the batch, and a slot
@@ -1080,22 +1186,15 @@ extern "C" thablasStatus_t thaDNN_q8_forward_batch(thablasHandle_t handle, int n
   if (!p || !w || !s_batch || !token || !pos || !logits_host || n_batches <= 0) return THABLAS_STATUS_INVALID_VALUE;
   int dev = 0;
   CHECK_HIP(hipGetDevice(&dev));
-  DecKey key(dev, handle.calc_stream, (const void*)w->wq, (const void*)s_batch->key_cache, (const void*)s_batch->x,
-             n_batches, p->dim, p->n_layers, p->seq_len, -p->vocab_size - 1 /* int8 keyspace */);
+  DecKey key(dev, handle.calc_stream, n_batches, p->dim, p->hidden_dim, p->n_layers, p->n_heads, p->n_kv_heads,
+             p->seq_len, -(p->vocab_size < 0 ? -p->vocab_size : p->vocab_size) - 1 /* int8 keyspace */);
   thallama_decoder* d = nullptr;
   {
     std::lock_guard<std::mutex> g(g_dec_mu);
-    auto it = dec_cache().find(key);
-    if (it != dec_cache().end()) {
-      d = it->second;
-      d->w8 = *w;
-      d->s = *s_batch;
-    } else {
-      if (thallama_decoder_create_q8(&d, p, w, s_batch, n_batches, handle.calc_stream) != 0) {
-        fprintf(stderr, "thaDNN_q8_forward_batch: %s\n", thallama_last_error());
-        return THABLAS_STATUS_INVALID_VALUE;
-      }
-      dec_cache()[key] = d;
+    d = dec_lookup(key, p, nullptr, w, s_batch, n_batches, handle.calc_stream);
+    if (!d) {
+      fprintf(stderr, "thaDNN_q8_forward_batch: %s\n", thallama_last_error());
+      return THABLAS_STATUS_INVALID_VALUE;
     }
   }
   const int r = thallama_decoder_forward(d, token, pos, logits_host);

@@ -1,5 +1,6 @@
 // gemv.hip — instantiations and launcher of the decode GEMV (see gemv.hpp).
 #include "gemv_dispatch.hpp"
+#include "gemv_launch.hpp"
 
 namespace tl {
 
@@ -16,6 +17,8 @@ bool gemv_fast_ok(const GemvParams& p) {
   if (p.rms_w && !al16(p.rms_w)) return false;
   return true;
 }
+
+bool gemv_matrix_path(const GemvParams& p) { return matrix_path_ok(p); }
 
 // Measured on MI355X (profiles/r01_gemv_sweep.json, llama2-7B shapes, weights streamed
 // from HBM): prefetch-before-staging costs 64 VGPRs and loses occupancy everywhere

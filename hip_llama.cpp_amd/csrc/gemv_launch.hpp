@@ -112,6 +112,16 @@ inline hipError_t launch_nb(const GemvParams& p, hipStream_t s, const GemvCfg& c
   return hipGetLastError();
 }
 
+// The shape half of the matrix-core / register-resident selection (the norm half is the
+// prologue test in launch_mode): whole 1-KiB wave-loads, 16-float k steps, aligned rows, and
+// at least gemv_mfma_min_nb() sequences in every 16-sequence group launch_mode cuts.
+inline bool matrix_path_ok(const GemvParams& p) {
+  if (p.n_items <= 0 || p.nb <= 0 || !gemv_fast_ok(p) || (p.K & 15) || (p.x_stride & 3)) return false;
+  for (int b0 = 0; b0 < p.nb; b0 += 16)
+    if ((p.nb - b0 < 16 ? p.nb - b0 : 16) < gemv_mfma_min_nb()) return false;
+  return true;
+}
+
 template <int MODE>
 inline hipError_t launch_mode(const GemvParams& p0, hipStream_t s, const GemvCfg* cfg, bool nt) {
   if (p0.n_items <= 0 || p0.nb <= 0) return hipSuccess;
@@ -137,8 +147,10 @@ inline hipError_t launch_mode(const GemvParams& p0, hipStream_t s, const GemvCfg
     }
     const GemvCfg c = cfg ? *cfg : gemv_default_cfg(MODE, p.n_items, p.K, p.nb, nt);
     hipError_t e;
-    if (!cfg && p.nb >= gemv_mfma_min_nb() && (p.K & 15) == 0 && (p.x_stride & 3) == 0 &&
-        ((!p.rms_w && !p.tok) || p.xn || (p.rms_w && p.ssq_in && !p.tok))) {
+    const bool matrix = !cfg && matrix_path_ok(p) &&
+                        ((!p.rms_w && !p.tok) || p.xn || (p.rms_w && p.ssq_in && !p.tok));
+    if (!matrix) p.ssq_in = nullptr;  // the streaming kernels normalise from x themselves
+    if (matrix) {
       // several sequences: the matrix-core kernel (gemv_mfma.hpp); an embedding prologue, or a
       // norm whose sums of squares the previous launch did not leave (ssq_in), runs once into
       // the scratch rows first; otherwise the kernel applies the norm itself

@@ -47,7 +47,7 @@ def sum_over_ranks(value, device=None):
 
 
 def serve_sharded(requests_path, out_path, tokenizer_path, vocab_size, batch, step, max_token_len, max_seq_len,
-                  temperature=None, topp=0.9, prefill=None, workdir="."):
+                  temperature=None, topp=0.9, prefill=None, workdir=".", native=None, outputs=None):
     """The reference's test mode (test_data_parallelism, src/llama.cpp:891-1083) with one process
     per GPU instead of one thread per GPU: every rank parses the request file
     (read_inputfile, src/llama.cpp:424-453), serves the contiguous shard :func:`shard` gives it
@@ -56,7 +56,10 @@ def serve_sharded(requests_path, out_path, tokenizer_path, vocab_size, batch, st
     the generated strings in request order and writes the output file (write_outputfile,
     src/llama.cpp:455-505).  Every request is sampled independently (seed 314028 each), so the
     file equals the single-process one byte for byte.  Returns the reference's num_gen_tokens
-    summed over ranks.  The only collectives are the object gather and that sum."""
+    summed over ranks.  The only collectives are the object gather and that sum.
+    ``native`` = (step address, prefill address or 0, ctx) drives the scheduler with native
+    callbacks instead of ``step`` / ``prefill`` (host.Requests.serve_native).  On rank 0 the
+    gathered responses (bytes, request order) are appended to ``outputs`` when it is a list."""
     import os
 
     from . import host as H
@@ -78,7 +81,10 @@ def serve_sharded(requests_path, out_path, tokenizer_path, vocab_size, batch, st
             os.remove(part)
         if temperature is not None:
             r.set_sampling(temperature, topp)
-        gen = r.serve(tokenizer_path, vocab_size, 1, batch, step, prefill)
+        if native is not None:
+            gen = r.serve_native(tokenizer_path, vocab_size, 1, batch, *native)
+        else:
+            gen = r.serve(tokenizer_path, vocab_size, 1, batch, step, prefill)
         outs = [r.output(i) for i in range(len(mine))]
     if world > 1:
         parts = [None] * world
@@ -88,4 +94,6 @@ def serve_sharded(requests_path, out_path, tokenizer_path, vocab_size, batch, st
     if rank == 0:
         with open(out_path, "wb") as f:
             f.write(f"{n}\n".encode() + b"".join(o + b"\n" for o in outs))
+        if outputs is not None:
+            outputs.extend(outs)
     return gen

@@ -171,6 +171,18 @@ class Requests:
             raise RuntimeError(f"serve_requests failed: {st}")
         return gen.value
 
+    def serve_native(self, tokenizer_path, vocab_size, n_workers, batch, step_addr, prefill_addr, ctx):
+        """Same scheduler driven by native callbacks (addresses of a thallama_step_fn and an optional
+        thallama_prefill_fn, e.g. libthallama's thallama_decoder_step_cb / _prefill_cb with ctx = the
+        decoder): no Python on the per-step path."""
+        gen = C.c_longlong(0)
+        st = lib().thallama_serve_requests_prefill(self.h, tokenizer_path.encode(), vocab_size, n_workers, batch,
+                                                  STEP_FN(step_addr), PREFILL_FN(prefill_addr) if prefill_addr
+                                                  else PREFILL_FN(), C.c_void_p(ctx), C.byref(gen))
+        if st:
+            raise RuntimeError(f"serve_requests failed: {st}")
+        return gen.value
+
     def __del__(self):
         if getattr(self, "h", None):
             lib().thallama_requests_free(self.h)

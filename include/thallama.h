@@ -99,6 +99,12 @@ int thallama_decoder_greedy(thallama_decoder* d, const int* token0_h, const int*
  * 64/128/256 (callers then feed the prompt token by token).  Synchronous. */
 int thallama_decoder_prefill(thallama_decoder* d, int b, const int* tokens_h, int n, int pos0);
 
+/* The decoder as the host scheduler's callbacks (include/thallama_host.h thallama_step_fn /
+ * thallama_prefill_fn, ctx = the decoder; worker ignored): step = thallama_decoder_forward,
+ * prefill = thallama_decoder_prefill (1 = not supported, negative = error). */
+int thallama_decoder_step_cb(void* ctx, int worker, int batch, const int* token, const int* pos, float* logits);
+int thallama_decoder_prefill_cb(void* ctx, int worker, int slot, const int* tokens, int n, int pos0);
+
 /* Copy the device logits of the last step into logits_h[batch*vocab] (synchronous). */
 int thallama_decoder_logits(thallama_decoder* d, float* logits_h);
 
@@ -109,6 +115,13 @@ int thallama_decoder_sync(thallama_decoder* d);
  * since the last reset. */
 int thallama_decoder_prof(thallama_decoder* d, int kclass, double* total_ms, long long* count);
 void thallama_decoder_prof_reset(thallama_decoder* d);
+
+/* thaDNN_s_forward_batch / thaDNN_q8_forward_batch keep one decoder per (device, stream, batch,
+ * config, dtype), made for the caller's weight and state buffers; a call with other buffers
+ * replaces it, and at most 8 live at once (least recently used freed).  The count, and a way to
+ * free them all (e.g. before the caller frees its buffers). */
+int thallama_forward_batch_cache_size(void);
+void thallama_forward_batch_cache_clear(void);
 
 /* Algorithmic HBM bytes of one step for kernel class kclass at the given positions
  * (weights once + KV rows read/written), used for roofline reporting. */

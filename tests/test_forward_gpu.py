@@ -127,6 +127,48 @@ def test_forward_batch_c_abi(gpu, oracle):
             assert_ref_close(logits[b * cfg[5]:(b + 1) * cfg[5]], ref[b].forward(toks[b][p], p), 1e-4, "abi")
 
 
+def test_forward_batch_decoder_cache_bounded(gpu, oracle):
+    """thaDNN_s_forward_batch keeps one decoder per (device, stream, batch, config): a caller that
+    reallocates its RunState every call does not grow the cache, the decoder follows the new
+    buffers, and distinct batch sizes stay within the cap of 8."""
+    cfg = SMALL
+    c = gpu.Config.make(*cfg)
+    model = gpu.DeviceModel(c, 0, seed=78)
+    h = gpu.new_handle()
+    gpu.lib().thallama_forward_batch_cache_clear()
+    logits = np.zeros(cfg[5], np.float32)
+    toks = [1, 7, 300, 5, 9]
+    prev = None
+    for p in range(len(toks)):
+        state = gpu.DeviceState(c, 1)  # a fresh state for every prefix: the cached decoder is replaced
+        want = oracle.Model(cfg, 0, seed=78)
+        for q in range(p + 1):
+            rc = gpu.lib().thaDNN_s_forward_batch(h, h, h, 1, C.byref(c), C.byref(model.w), state.ptr,
+                                                  (C.c_int * 1)(toks[q]), (C.c_int * 1)(q),
+                                                  logits.ctypes.data_as(gpu.c_float_p))
+            assert rc == 0
+            lw = want.forward(toks[q], q)
+        assert_ref_close(logits, lw, 1e-4, f"fresh state, prefix {p}")
+        assert gpu.lib().thallama_forward_batch_cache_size() == 1
+        if prev is not None:
+            prev.free()
+        prev = state
+    gpu.lib().thallama_forward_batch_cache_clear()
+    prev.free()
+    keep = []
+    for B in range(1, 12):
+        st = gpu.DeviceState(c, B)
+        keep.append(st)
+        lg = np.zeros(B * cfg[5], np.float32)
+        rc = gpu.lib().thaDNN_s_forward_batch(h, h, h, B, C.byref(c), C.byref(model.w), st.ptr,
+                                              (C.c_int * B)(*([1] * B)), (C.c_int * B)(*([0] * B)),
+                                              lg.ctypes.data_as(gpu.c_float_p))
+        assert rc == 0
+        assert gpu.lib().thallama_forward_batch_cache_size() == min(B, 8)
+    gpu.lib().thallama_forward_batch_cache_clear()
+    assert gpu.lib().thallama_forward_batch_cache_size() == 0
+
+
 @pytest.mark.parametrize("token,pos", [(0, 0), (3, 4), (4, 4), (64, 64)])
 def test_stories110m_reference_cases(gpu, oracle, token, pos):
     """The reference's own forward test points (scripts/test/thaDNN.test.cpp:541-549) on a
@@ -165,6 +207,32 @@ def test_llama2_7b_shape(gpu, oracle):
         assert_ref_close(got, want, 1e-4, f"7B logits pos {p}")
         assert int(np.argmax(got)) == int(np.argmax(want))
         toks.append(int(np.argmax(want)))
+
+
+@pytest.mark.parametrize("B", [4, 8])
+@pytest.mark.parametrize("abi", [0, 1])
+def test_batched_norm_carry_mixed_paths(gpu, oracle, B, abi):
+    """dim % 256 == 0 but hidden % 256 != 0 (stories42M-like 512 / 1376): W2 (K = hidden) takes the
+    generic GEMV, which leaves no RMSNorm sums, while QKV / W1-W3 / the classifier (K = dim) take
+    the matrix-core kernel — the sums must then not be carried across launches (round-2 review).
+    Teacher-forced random tokens through the decoder and through thaDNN_s_forward_batch."""
+    cfg = (512, 1376, 3, 8, 8, 1024, 64)
+    c, model, state, dec, _ = build(gpu, oracle, cfg, 0, seed=42, batch=B)
+    refs = [oracle.Model(cfg, 0, seed=42) for _ in range(B)]
+    toks = np.random.default_rng(B + 10 * abi).integers(0, cfg[5], (B, 6))
+    h = gpu.new_handle()
+    logits = np.zeros(B * cfg[5], np.float32)
+    for p in range(6):
+        if abi:
+            tk = (C.c_int * B)(*toks[:, p].tolist())
+            ps = (C.c_int * B)(*([p] * B))
+            assert gpu.lib().thaDNN_s_forward_batch(h, h, h, B, C.byref(c), C.byref(model.w), state.ptr, tk, ps,
+                                                    logits.ctypes.data_as(gpu.c_float_p)) == 0
+            got = logits.reshape(B, cfg[5])
+        else:
+            got = dec.forward(toks[:, p].tolist(), [p] * B)
+        for b in range(B):
+            assert_ref_close(got[b], refs[b].forward(int(toks[b, p]), p), 1e-4, f"B={B} b={b} pos={p}")
 
 
 @pytest.mark.parametrize("B", [4, 7, 16, 17])
