@@ -74,6 +74,8 @@ def parse_args(argv):
                     help="multi-launch step instead of the one-launch persistent step")
     ap.add_argument("--no-long", action="store_true", help="skip the positions 1792..2047 line")
     ap.add_argument("--no-requests-point", action="store_true", help="skip the 1-GPU request-workload point")
+    ap.add_argument("--host-argmax", action="store_true",
+                    help="requests: greedy sampling on the host from copied logits (the reference's way)")
     ap.add_argument("--write-fixture", action="store_true",
                     help="requests: serve all 64 prompts in this process and write the output fixture")
     ap.add_argument("--cpu-baseline-tokens", type=int, default=0,
@@ -372,8 +374,10 @@ def main(argv=None):
         prompt_pos = sum(max(0, min(len(tok.encode(p)), T) - 1) for p in prompts)  # prefilled / forced positions
         mtl = tok.max_token_length
         tok.close()
-        native = (tl.C.cast(tl.lib().thallama_decoder_step_cb, tl.C.c_void_p).value,
-                  tl.C.cast(tl.lib().thallama_decoder_prefill_cb, tl.C.c_void_p).value, dec.h.value)
+        addr = lambda f: tl.C.cast(f, tl.C.c_void_p).value  # noqa: E731
+        # step (logits), prefill, decoder, greedy step (device argmax: B ids back instead of B x V logits)
+        native = (addr(tl.lib().thallama_decoder_step_cb), addr(tl.lib().thallama_decoder_prefill_cb), dec.h.value,
+                  0 if args.host_argmax else addr(tl.lib().thallama_decoder_argmax_cb))
         gen, outs = [0], []
 
         def one():

@@ -199,6 +199,7 @@ static std::vector<Replica> replicate(ModelFile& m, int n_dev, int n_rep, int ba
       fprintf(stderr, "decoder on device %d: %s\n", d, thallama_last_error());
       exit(EXIT_FAILURE);
     }
+    thallama_decoder_set(r.dec, THALLAMA_OPT_USE_GRAPH, 1);  // each step replayed as one captured graph
   }
   return reps;
 }
@@ -222,6 +223,16 @@ static int replica_step(void* ctx, int worker, int batch, const int* token, cons
   if (hipSetDevice(r.dev) != hipSuccess) return -3;
   (void)batch;
   const int st = thallama_decoder_forward(r.dec, token, pos, logits);
+  if (st) fprintf(stderr, "device %d step: %s\n", r.dev, thallama_last_error());
+  return st;
+}
+
+// greedy test mode (-g 1): the argmax stays on the device and only the batch's ids come back
+static int replica_argmax(void* ctx, int worker, int batch, const int* token, const int* pos, int* next) {
+  Replica& r = (*(std::vector<Replica>*)ctx)[worker];
+  if (hipSetDevice(r.dev) != hipSuccess) return -3;
+  (void)batch;
+  const int st = thallama_decoder_step_argmax(r.dec, token, pos, next);
   if (st) fprintf(stderr, "device %d step: %s\n", r.dev, thallama_last_error());
   return st;
 }
@@ -376,8 +387,9 @@ int main(int argc, char* argv[]) {
 
     const long start = time_in_ms();
     long long num_gen_tokens = 0;
-    const int st = thallama_serve_requests_prefill(req, tokenizer_path, V, n_rep, batch, replica_step, replica_prefill,
-                                                   &reps, &num_gen_tokens);
+    const int st = thallama_serve_requests_greedy(req, tokenizer_path, V, n_rep, batch, replica_step,
+                                                  getenv("THALLAMA_HOST_ARGMAX") ? nullptr : replica_argmax,
+                                                  replica_prefill, &reps, &num_gen_tokens);
     const long end = time_in_ms();
     if (st != 0) {
       fprintf(stderr, "test mode failed (%d)\n", st);

@@ -122,6 +122,7 @@ struct thallama_decoder {
   int* out_d = nullptr;  // [B][S] greedy tokens by position
   int* tok_h = nullptr;  // pinned staging
   int* pos_h = nullptr;
+  int* nxt_h = nullptr;  // pinned: argmax ids of a greedy step
   float2* rope_d = nullptr;
   float* xn_d = nullptr;        // [<=16][dim] normed rows for the matrix-core GEMV (batch >= 2)
   float* ssq_d = nullptr;       // [B][dim/16] per-tile sums of squares carried from Wo / W2 to the next norm
@@ -279,6 +280,7 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
   TL_TRY(hipMalloc(&d->out_d, sizeof(int) * (size_t)batch * d->S));
   TL_TRY(hipHostMalloc(&d->tok_h, sizeof(int) * batch, hipHostMallocDefault));
   TL_TRY(hipHostMalloc(&d->pos_h, sizeof(int) * batch, hipHostMallocDefault));
+  TL_TRY(hipHostMalloc(&d->nxt_h, sizeof(int) * batch, hipHostMallocDefault));
   // RoPE table with the reference's exact host formula (src/seq.cpp:88-92), so the
   // device rotation uses bit-identical cos/sin.
   std::vector<float2> rope((size_t)d->S * (d->hs / 2));
@@ -348,6 +350,7 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   (void)hipFree(d->out_d);
   (void)hipHostFree(d->tok_h);
   (void)hipHostFree(d->pos_h);
+  (void)hipHostFree(d->nxt_h);
   (void)hipFree(d->rope_d);
   (void)hipFree(d->xn_d);
   (void)hipFree(d->ssq_d);
@@ -843,6 +846,62 @@ static int decoder_forward_once(thallama_decoder* d, const int* token_h, const i
 static int decoder_greedy_once(thallama_decoder* d, const int* token0_h, const int* pos0_h, int n_steps,
                                int* tokens_out_h, int sync);
 
+// One greedy step (the step + the argmax that feeds tok/pos) captured as a graph, once.
+static int ensure_greedy_graph(thallama_decoder* d) {
+  if (d->exec) return 0;
+  hipGraph_t g = nullptr;
+  TL_TRY(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
+  int e = 0;
+  if (use_persist(d)) {
+    e = enqueue_persistent(d, true);
+  } else {
+    e = enqueue_step(d);
+    if (!e) e = enqueue_argmax(d);
+  }
+  hipError_t ce = hipStreamEndCapture(d->stream, &g);
+  if (e) return e;
+  TL_TRY(ce);
+  TL_TRY(hipGraphInstantiate(&d->exec, g, nullptr, nullptr, 0));
+  (void)hipGraphDestroy(g);
+  return 0;
+}
+
+// One greedy step with host token/pos: next_h[b] = the device argmax of slot b's logits (the
+// scheduler's greedy step, thallama_argmax_step_fn).  B ids come back instead of B x V logits.
+static int decoder_step_argmax_once(thallama_decoder* d, const int* token_h, const int* pos_h, int* next_h) {
+  if (!d || !token_h || !pos_h || !next_h) return (int)hipErrorInvalidValue;
+  int r = upload_tok_pos(d, token_h, pos_h);
+  if (r) return r;
+  if (d->use_graph && !d->profile) {
+    if ((r = ensure_greedy_graph(d)) != 0) return r;
+    TL_TRY(hipGraphLaunch(d->exec, d->stream));
+  } else {
+    r = use_persist(d) ? enqueue_persistent(d, true) : enqueue_step(d);
+    if (!r && !use_persist(d)) r = enqueue_argmax(d);
+    if (r) return r;
+  }
+  TL_TRY(hipMemcpyAsync(d->nxt_h, d->tok_d, sizeof(int) * d->B, hipMemcpyDeviceToHost, d->stream));
+  TL_TRY(hipStreamSynchronize(d->stream));
+  memcpy(next_h, d->nxt_h, sizeof(int) * d->B);
+  prof_collect(d);
+  return check_persist(d);
+}
+
+extern "C" int thallama_decoder_step_argmax(thallama_decoder* d, const int* token_h, const int* pos_h, int* next_h) {
+  const bool persistent = d && use_persist(d);
+  int r = decoder_step_argmax_once(d, token_h, pos_h, next_h);
+  if (r == kPersistFellBack && persistent && !use_persist(d)) r = decoder_step_argmax_once(d, token_h, pos_h, next_h);
+  return r;
+}
+
+extern "C" int thallama_decoder_argmax_cb(void* ctx, int worker, int batch, const int* token, const int* pos,
+                                          int* next) {
+  (void)worker;
+  thallama_decoder* d = (thallama_decoder*)ctx;
+  if (!d || batch != d->B) return (int)hipErrorInvalidValue;
+  return thallama_decoder_step_argmax(d, token, pos, next);
+}
+
 extern "C" int thallama_decoder_greedy(thallama_decoder* d, const int* token0_h, const int* pos0_h, int n_steps,
                                        int* tokens_out_h, int sync) {
   const bool persistent = d && use_persist(d);
@@ -863,22 +922,7 @@ static int decoder_greedy_once(thallama_decoder* d, const int* token0_h, const i
   int r = upload_tok_pos(d, token0_h, pos0_h);
   if (r) return r;
   const bool graph = d->use_graph && !d->profile;
-  if (graph && !d->exec) {
-    hipGraph_t g = nullptr;
-    TL_TRY(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
-    int e = 0;
-    if (use_persist(d)) {
-      e = enqueue_persistent(d, true);
-    } else {
-      e = enqueue_step(d);
-      if (!e) e = enqueue_argmax(d);
-    }
-    hipError_t ce = hipStreamEndCapture(d->stream, &g);
-    if (e) return e;
-    TL_TRY(ce);
-    TL_TRY(hipGraphInstantiate(&d->exec, g, nullptr, nullptr, 0));
-    (void)hipGraphDestroy(g);
-  }
+  if (graph && (r = ensure_greedy_graph(d)) != 0) return r;
   for (int i = 0; i < n_steps; ++i) {
     if (graph) {
       TL_TRY(hipGraphLaunch(d->exec, d->stream));

@@ -11,6 +11,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 STEP_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
                       C.POINTER(C.c_float))
 PREFILL_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int), C.c_int, C.c_int)
+ARGMAX_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                        C.POINTER(C.c_int))
 
 
 def lib():
@@ -51,6 +53,8 @@ def lib():
             "thallama_serve_requests": (I, [VP, S, I, I, I, STEP_FN, VP, C.POINTER(C.c_longlong)]),
             "thallama_serve_requests_prefill": (I, [VP, S, I, I, I, STEP_FN, PREFILL_FN, VP,
                                                     C.POINTER(C.c_longlong)]),
+            "thallama_serve_requests_greedy": (I, [VP, S, I, I, I, STEP_FN, ARGMAX_FN, PREFILL_FN, VP,
+                                                   C.POINTER(C.c_longlong)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -171,14 +175,18 @@ class Requests:
             raise RuntimeError(f"serve_requests failed: {st}")
         return gen.value
 
-    def serve_native(self, tokenizer_path, vocab_size, n_workers, batch, step_addr, prefill_addr, ctx):
-        """Same scheduler driven by native callbacks (addresses of a thallama_step_fn and an optional
-        thallama_prefill_fn, e.g. libthallama's thallama_decoder_step_cb / _prefill_cb with ctx = the
-        decoder): no Python on the per-step path."""
+    def serve_native(self, tokenizer_path, vocab_size, n_workers, batch, step_addr, prefill_addr, ctx,
+                     argmax_addr=0):
+        """Same scheduler driven by native callbacks (addresses of a thallama_step_fn, an optional
+        thallama_prefill_fn and an optional thallama_argmax_step_fn used for greedy sampling, e.g.
+        libthallama's thallama_decoder_step_cb / _prefill_cb / _argmax_cb with ctx = the decoder):
+        no Python on the per-step path."""
         gen = C.c_longlong(0)
-        st = lib().thallama_serve_requests_prefill(self.h, tokenizer_path.encode(), vocab_size, n_workers, batch,
-                                                  STEP_FN(step_addr), PREFILL_FN(prefill_addr) if prefill_addr
-                                                  else PREFILL_FN(), C.c_void_p(ctx), C.byref(gen))
+        st = lib().thallama_serve_requests_greedy(self.h, tokenizer_path.encode(), vocab_size, n_workers, batch,
+                                                 STEP_FN(step_addr) if step_addr else STEP_FN(),
+                                                 ARGMAX_FN(argmax_addr) if argmax_addr else ARGMAX_FN(),
+                                                 PREFILL_FN(prefill_addr) if prefill_addr else PREFILL_FN(),
+                                                 C.c_void_p(ctx), C.byref(gen))
         if st:
             raise RuntimeError(f"serve_requests failed: {st}")
         return gen.value

@@ -308,7 +308,18 @@ extern "C" int thallama_serve_requests(thallama_requests* r, const char* tokeniz
 extern "C" int thallama_serve_requests_prefill(thallama_requests* r, const char* tokenizer_path, int vocab_size,
                                                int n_workers, int batch, thallama_step_fn step,
                                                thallama_prefill_fn prefill, void* ctx, long long* gen_tokens) {
-  if (!r || !step || n_workers <= 0 || batch <= 0) return -1;
+  return thallama_serve_requests_greedy(r, tokenizer_path, vocab_size, n_workers, batch, step, nullptr, prefill, ctx,
+                                        gen_tokens);
+}
+
+extern "C" int thallama_serve_requests_greedy(thallama_requests* r, const char* tokenizer_path, int vocab_size,
+                                              int n_workers, int batch, thallama_step_fn step,
+                                              thallama_argmax_step_fn argmax_step, thallama_prefill_fn prefill,
+                                              void* ctx, long long* gen_tokens) {
+  if (!r || n_workers <= 0 || batch <= 0) return -1;
+  // greedy sampling is sample_argmax of the logits: the device step may take it (only B ids return)
+  const bool on_device = argmax_step && r->temperature == 0.0f;
+  if (!on_device && !step) return -1;
   const int n_req = (int)r->prompts.size();
   const int V = vocab_size;
   std::vector<thallama_sampler*> samplers((size_t)n_req);
@@ -324,7 +335,8 @@ extern "C" int thallama_serve_requests_prefill(thallama_requests* r, const char*
       status = -2;
       return;
     }
-    std::vector<float> logits((size_t)batch * V);
+    std::vector<float> logits(on_device ? 0 : (size_t)batch * V);
+    std::vector<int> next_ids(batch, 0);
     std::vector<int> req(batch, -1), token(batch, 0), pos(batch, 0), steps(batch, 0), n_prompt(batch, 0);
     std::vector<char> done(batch, 0);
     std::vector<std::vector<int>> prompt(batch);
@@ -379,7 +391,8 @@ extern "C" int thallama_serve_requests_prefill(thallama_requests* r, const char*
       }
       if (status != 0) break;
       if (idle == batch) break;
-      const int st = step(ctx, w, batch, token.data(), pos.data(), logits.data());
+      const int st = on_device ? argmax_step(ctx, w, batch, token.data(), pos.data(), next_ids.data())
+                               : step(ctx, w, batch, token.data(), pos.data(), logits.data());
       if (st != 0) {
         status = st;
         break;
@@ -388,6 +401,7 @@ extern "C" int thallama_serve_requests_prefill(thallama_requests* r, const char*
         if (req[b] < 0) continue;
         int next;
         if (pos[b] < n_prompt[b] - 1) next = prompt[b][pos[b] + 1];  // still in the prompt
+        else if (on_device) next = next_ids[b];
         else next = thallama_sample(samplers[req[b]], logits.data() + (size_t)b * V);
         pos[b] += 1;
         if (next == 1 || next == 2) {  // BOS / EOS end the sequence

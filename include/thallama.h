@@ -104,6 +104,11 @@ int thallama_decoder_prefill(thallama_decoder* d, int b, const int* tokens_h, in
  * prefill = thallama_decoder_prefill (1 = not supported, negative = error). */
 int thallama_decoder_step_cb(void* ctx, int worker, int batch, const int* token, const int* pos, float* logits);
 int thallama_decoder_prefill_cb(void* ctx, int worker, int slot, const int* tokens, int n, int pos0);
+/* One greedy step with host token/pos whose argmax stays on the device: next_h[b] = the first
+ * index of the maximum of slot b's logits (sample_argmax, src/llama.cpp:275-286); only the B ids
+ * are copied back.  Synchronous.  And as thallama_argmax_step_fn (include/thallama_host.h). */
+int thallama_decoder_step_argmax(thallama_decoder* d, const int* token_h, const int* pos_h, int* next_h);
+int thallama_decoder_argmax_cb(void* ctx, int worker, int batch, const int* token, const int* pos, int* next);
 
 /* Copy the device logits of the last step into logits_h[batch*vocab] (synchronous). */
 int thallama_decoder_logits(thallama_decoder* d, float* logits_h);

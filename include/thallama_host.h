@@ -82,6 +82,16 @@ typedef int (*thallama_prefill_fn)(void* ctx, int worker, int slot, const int* t
 int thallama_serve_requests_prefill(thallama_requests* r, const char* tokenizer_path, int vocab_size,
                                     int n_workers, int batch, thallama_step_fn step, thallama_prefill_fn prefill,
                                     void* ctx, long long* gen_tokens);
+/* A greedy decode step that samples on the device: token[b] at pos[b] -> next[b] = the argmax of
+ * slot b's logits with sample_argmax's rule (first index of the maximum, src/llama.cpp:275-286).
+ * Only B ids cross to the host instead of B x V logits.  Returns 0 on success. */
+typedef int (*thallama_argmax_step_fn)(void* ctx, int worker, int batch, const int* token, const int* pos, int* next);
+/* thallama_serve_requests_prefill where, for greedy sampling (temperature 0), `argmax_step` (when
+ * non-null) replaces `step`: same outputs and *gen_tokens, since greedy sampling is that argmax.
+ * With another temperature `step` runs as before (it must then be non-null). */
+int thallama_serve_requests_greedy(thallama_requests* r, const char* tokenizer_path, int vocab_size, int n_workers,
+                                   int batch, thallama_step_fn step, thallama_argmax_step_fn argmax_step,
+                                   thallama_prefill_fn prefill, void* ctx, long long* gen_tokens);
 
 #ifdef __cplusplus
 }
