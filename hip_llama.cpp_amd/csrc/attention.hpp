@@ -219,10 +219,11 @@ TL_DEVICE void store_head(const AttnWaveParams& w, int b, int h, const float* v,
 // Persistent step (fp32 weights): publish head h's output row (lane holds columns lane*VPL + c)
 // as {value, tag} granules.
 template <int HS>
-TL_DEVICE void publish_head(const AttnWaveParams& w, int h, const float* v, int lane) {
+TL_DEVICE void publish_head(const AttnWaveParams& w, int b, int h, const float* v, int lane) {
   constexpr int VPL = HS / 64;
+  unsigned long long* go = w.gout + (long long)b * w.a.dim;  // sequence b's row (batched step)
 #pragma unroll
-  for (int c = 0; c < VPL; ++c) st8_sc1(w.gout + h * HS + lane * VPL + c, gran(w.tag_out, v[c]));
+  for (int c = 0; c < VPL; ++c) st8_sc1(go + h * HS + lane * VPL + c, gran(w.tag_out, v[c]));
 }
 
 // The body of one attention unit, run by one full wave; `unit` must be wave-uniform.  Also used
@@ -255,7 +256,9 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
   // first chunk's cached rows are in flight
   __amdgpu_buffer_rsrc_t rg;
   bool qready = false;
-  if constexpr (GR) rg = rsrc_of(w.gqkv);
+  // sequence b's q | k_new | v_new granules (the batched persistent step keeps B rows)
+  const unsigned long long* gq = w.gqkv + (long long)b * (p.dim + 2 * p.kv_dim);
+  if constexpr (GR) rg = rsrc_of(gq);
   else qv = reinterpret_cast<const f4*>(qrow)[lane % LPK];
   const float rs = sqrtf((float)HS);
   const bool whole = nchunks == 1;
@@ -305,7 +308,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
           ka = ld16_sc1(rg, ko);
           kb = ld16_sc1(rg, ko + 16);
 #pragma unroll
-          for (int c = 0; c < VPL; ++c) vr[c] = ld8_sc1(w.gqkv + vo / 8 + c);
+          for (int c = 0; c < VPL; ++c) vr[c] = ld8_sc1(gq + vo / 8 + c);
         }
         qv = gran4_ok(qa, qb, w.tag_in) ? gran4_val(qa, qb) : gran_wait4(rg, qo, w.tag_in, w.err);
         qready = true;
@@ -315,7 +318,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
 #pragma unroll
           for (int c = 0; c < VPL; ++c)
             vn[c] = (unsigned)(vr[c] >> 32) == w.tag_in ? __uint_as_float((unsigned)vr[c])
-                                                       : gran_wait(w.gqkv + vo / 8 + c, w.tag_in, w.err);
+                                                       : gran_wait(gq + vo / 8 + c, w.tag_in, w.err);
           kvready = true;
         }
       }
@@ -323,7 +326,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
         if (!kvready) {
           kn = gran_wait4(rg, ko, w.tag_in, w.err);
 #pragma unroll
-          for (int c = 0; c < VPL; ++c) vn[c] = gran_wait(w.gqkv + vo / 8 + c, w.tag_in, w.err);
+          for (int c = 0; c < VPL; ++c) vn[c] = gran_wait(gq + vo / 8 + c, w.tag_in, w.err);
         }
         if (w.ts && lane == 0) w.ts[1] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
@@ -393,7 +396,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
   if (whole) {
     if constexpr (GR) {
       if (w.ts && lane == 0) w.ts[2] = __builtin_amdgcn_s_memrealtime();
-      publish_head<HS>(w, h, o, lane);
+      publish_head<HS>(w, b, h, o, lane);
     } else {
       store_head<HS>(w, b, h, o, lane);
     }
@@ -442,7 +445,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
 #pragma unroll
   for (int c = 0; c < VPL; ++c) acc[c] = __fdiv_rn(acc[c], L);
   if constexpr (GR) {
-    publish_head<HS>(w, h, acc, lane);
+    publish_head<HS>(w, b, h, acc, lane);
   } else {
     store_head<HS>(w, b, h, acc, lane);
   }

@@ -235,9 +235,20 @@ static int auto_splits(const thallama_decoder* d) {
   return ns;
 }
 
-// Hand-off granules of the persistent step: x | xb | hb | q k v | int8 attention scores [H][S].
+// Hand-off granules of the persistent step: x | xb | hb | q k v | int8 attention scores [H][S]
+// (batch 1); B rows of each of the first four for the batched step (persist_b.hip).
 static size_t granule_count(const thallama_decoder* d) {
+  if (d->B > 1) return (size_t)d->B * (3 * d->dim + d->hidden + 2 * d->kv_dim) + 2;
   return (size_t)3 * d->dim + d->hidden + 2 * d->kv_dim + (size_t)d->H * d->S + 2;
+}
+
+// The batched persistent step (2..8 sequences, fp32): on unless THALLAMA_BATCH_PERSIST=0.
+static bool batch_persist_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("THALLAMA_BATCH_PERSIST");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg, const TransformerWeights* w,
@@ -317,21 +328,25 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
   d->nt = wbytes > 1024.0 * 1024.0 * 1024.0;
   // persistent step: batch 1, fp32 (decided again for int8 in _create_q8)
   TL_TRY(hipDeviceGetAttribute(&d->ncu, hipDeviceAttributeMultiprocessorCount, d->dev));
-  if (batch == 1) {
+  {
     tl::PStep ps = {};
     ps.dim = d->dim; ps.hid = d->hidden; ps.kvd = d->kv_dim; ps.hs = d->hs; ps.NS = d->nsplit;
-    ps.L = d->L; ps.H = d->H; ps.S = d->S; ps.V = d->V;
+    ps.L = d->L; ps.H = d->H; ps.S = d->S; ps.V = d->V; ps.B = batch;
     const char* why = nullptr;
-    d->pok = tl::persistent_prepare(ps, d->ncu, &why);
+    if (batch == 1) {
+      d->pok = tl::persistent_prepare(ps, d->ncu, &why);
+    } else if (batch <= 8 && batch_persist_enabled()) {
+      d->pok = tl::persistent_prepare_b(ps, d->ncu, &why);
+    } else {
+      why = batch > 8 ? "batch > 8" : "THALLAMA_BATCH_PERSIST=0";
+    }
     if (!d->pok && why) d->pwhy = why;
-  } else {
-    d->pwhy = "batch > 1";
   }
   if (d->pok) {
-    d->psync_zero = tl::kPSyncWords + (((size_t)d->L * d->H + 3) & ~(size_t)3);
+    d->psync_zero = tl::kPSyncWords + (((size_t)d->L * d->H * batch + 3) & ~(size_t)3);
     TL_TRY(hipMalloc(&d->psync, sizeof(unsigned) * (d->psync_zero + 32)));
     TL_TRY(hipMemset(d->psync, 0, sizeof(unsigned) * (d->psync_zero + 32)));
-    TL_TRY(hipMalloc(&d->pbmax, sizeof(unsigned long long) * d->ncu));
+    TL_TRY(hipMalloc(&d->pbmax, sizeof(unsigned long long) * d->ncu * (batch > 1 ? 8 : 1)));
     const size_t ng = granule_count(d);
     TL_TRY(hipMalloc(&d->pgran, sizeof(unsigned long long) * ng));
     TL_TRY(hipMemset(d->pgran, 0, sizeof(unsigned long long) * ng));
@@ -680,8 +695,12 @@ static int enqueue_persistent(thallama_decoder* d, bool argmax) {
   p.x = s.x; p.xb = s.xb; p.logits = s.logits; p.kc = s.key_cache; p.vc = s.value_cache;
   p.part = d->part_d; p.rope = d->rope_d;
   p.tok = d->tok_d; p.pos = d->pos_d; p.out = d->out_d;
-  p.gx = d->pgran; p.gxb = p.gx + d->dim; p.ghb = p.gxb + d->dim; p.gqkv = p.ghb + d->hidden;
-  p.gsc = p.gqkv + d->dim + 2 * d->kv_dim;
+  p.B = d->B;
+  {
+    const size_t B = d->B;  // B rows of each hand-off buffer (batch 1: one)
+    p.gx = d->pgran; p.gxb = p.gx + B * d->dim; p.ghb = p.gxb + B * d->dim; p.gqkv = p.ghb + B * d->hidden;
+    p.gsc = p.gqkv + B * (d->dim + 2 * d->kv_dim);
+  }
   p.sync = d->psync; p.tickets = d->psync + tl::kPSyncWords;
   p.err = d->psync + d->psync_zero; p.seq = p.err + 1; p.bmax = d->pbmax;
   p.argmax = argmax ? 1 : 0;
@@ -698,13 +717,13 @@ static int enqueue_persistent(thallama_decoder* d, bool argmax) {
     p.scls = d->w8.wcls->s;
   }
   const char* why = nullptr;
-  if (!tl::persistent_prepare(p, d->ncu, &why)) {
+  if (!(d->B > 1 ? tl::persistent_prepare_b(p, d->ncu, &why) : tl::persistent_prepare(p, d->ncu, &why))) {
     g_last_error = std::string("persistent step: ") + (why ? why : "unsupported");
     return (int)hipErrorInvalidValue;
   }
   TL_TRY(hipMemsetAsync(p.sync, 0, sizeof(unsigned) * d->psync_zero, d->stream));
   const int ev = prof_begin(d);
-  TL_TRY(tl::launch_persistent_step(p, d->stream, d->ncu));
+  TL_TRY(d->B > 1 ? tl::launch_persistent_step_b(p, d->stream, d->ncu) : tl::launch_persistent_step(p, d->stream, d->ncu));
   prof_end(d, THALLAMA_K_STEP, ev);
   return 0;
 }
@@ -1183,6 +1202,10 @@ extern "C" int thallama_decoder_create_q8(thallama_decoder** out, const Config* 
       TL_TRY(hipMalloc(&d->hcnt_d, sizeof(unsigned) * (size_t)(d->hidden / 64)));
       TL_TRY(hipMemset(d->hcnt_d, 0, sizeof(unsigned) * (size_t)(d->hidden / 64)));
     }
+  }
+  if (batch > 1 && d->pok) {  // the batched persistent step is fp32 only: int8 batches run multi-launch
+    d->pok = false;
+    d->pwhy = "int8 weights with batch > 1";
   }
   // persistent step with int8 weights: re-check the shape (group size, LDS) and publish the
   // per-layer tensor addresses as a device table the kernel indexes by (tensor, layer)

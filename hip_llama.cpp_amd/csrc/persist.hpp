@@ -43,6 +43,9 @@ struct PStep {
   int ang;                  // Q8: attention units per head (persistent_prepare)
   int fault;                // test hook (THALLAMA_OPT_PERSIST_FAULT): block 0 exits at once, as
                             // if the grid were not co-resident; every other wait gives up
+  int B;                    // batched step (persist_b.hip): 2..8 sequences; tok / pos / out and every
+                            // hand-off buffer then hold B rows, bmax [grid][8], tickets [L][B*H];
+                            // n_scr = the LDS row-chunk partials (persistent_prepare_b)
 };
 
 constexpr int kPSyncWords = 8 * 32;   // 8 shard counters, one 128-B line each
@@ -56,5 +59,8 @@ bool persistent_prepare(PStep& p, int ncu, const char** why);
 hipError_t launch_persistent_step(const PStep& p, hipStream_t s, int ncu);
 // True if launch_persistent_step uses a cooperative launch (co-residency guaranteed).
 bool persistent_cooperative();
+// The same for 2..8 sequences with fp32 weights (persist_b.hip; p.B set).
+bool persistent_prepare_b(PStep& p, int ncu, const char** why);
+hipError_t launch_persistent_step_b(const PStep& p, hipStream_t s, int ncu);
 
 }  // namespace tl

@@ -15,8 +15,9 @@ be no further from the CPU reference than the reference's own GPU implementation
 the count beyond 1e-4), every earlier token still identical; the 110M cases keep 1e-4.
 Cases: stories110M shape with a shared and an unshared classifier, and llama2-7B (the bench's own
 model: same seed), each on the persistent one-launch step, the multi-launch step, and — for the
-8-GPU config's per-GPU workload — 8 sequences at once on the matrix-core GEMV path, and 4 at once
-(at 7B the register-resident GEMV, gemv_rr.hpp).
+8-GPU config's per-GPU workload — 8 and 4 sequences at once, on the batched persistent step
+(persist_b.hip) and on the multi-launch batched step (matrix-core GEMV, gemv_mfma.hpp; at 7B and
+4 sequences the register-resident GEMV, gemv_rr.hpp).
 """
 import json
 import os
@@ -45,16 +46,18 @@ def fp32_decoder(tl, case, batch):
 
 
 @pytest.mark.parametrize("name", ["stories110m_shared", "stories110m_unshared", "llama2_7b"])
-@pytest.mark.parametrize("path", ["persistent", "multilaunch", "batch8", "batch4"])
+@pytest.mark.parametrize("path", ["persistent", "multilaunch", "batch8", "batch4", "batch8_multilaunch",
+                                  "batch4_multilaunch"])
 def test_fp32_256_step_greedy_equals_reference(gpu, name, path):
     case = CASES[name]
     g = case["fp32"]
-    B = {"batch8": 8, "batch4": 4}.get(path, 1)
+    B = 8 if path.startswith("batch8") else 4 if path.startswith("batch4") else 1
     keep, dec = fp32_decoder(gpu, case, B)
     dec.set(gpu.OPT_USE_GRAPH, 1)
-    if path == "multilaunch":
+    multi = path.endswith("multilaunch")
+    if multi:
         dec.set(gpu.OPT_PERSISTENT, 0)
-    assert dec.persistent() == (path == "persistent")
+    assert dec.persistent() == (not multi)  # batch 4 / 8: the batched persistent step (persist_b.hip)
     n = case["steps"]
     got = dec.greedy([case["start_token"]] * B, [case["start_pos"]] * B, n)
     for b in range(B):

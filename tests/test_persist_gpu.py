@@ -34,7 +34,10 @@ def test_selection(gpu):
         assert dec.persistent() == want, cfg
         dec.set(gpu.OPT_PERSISTENT, 0)
         assert not dec.persistent()
+    # 2..8 sequences: the batched persistent step (persist_b.hip, tests/test_persist_b_gpu.py)
     _, _, _, dec = decoder(gpu, SMALL, 0, 1, 1, batch=2)
+    assert dec.persistent()
+    _, _, _, dec = decoder(gpu, SMALL, 0, 1, 1, batch=9)
     assert not dec.persistent()
 
 
