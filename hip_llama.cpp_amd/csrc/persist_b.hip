@@ -11,13 +11,13 @@
 // this is the same engine for B sequences.
 //
 // What changes with B sequences:
-//  * The activations of every sequence are needed for each weight byte, but B x K floats do not
-//    fit the LDS for B = 8 (128 KiB at K = 4096, 344 KiB for W2's K = 11008).  So a GEMV phase
-//    runs in K-passes of one row chunk (KC = 2048 floats, 8 KiB of a row): pass c stages
-//    x[b][c*KC .. c*KC + KC) of every sequence (64 KiB at B = 8), then the streaming waves sweep
-//    chunk c of every row the block owns.  A slot is one 8-KiB row chunk, as in the batch-1 step,
-//    and its consume does B dot products with the staged strip (B ds_read_b128 per weight
-//    float4: ~40% of the LDS rate at the HBM stream rate, 8 sequences).
+//  * The activations of every sequence are needed for each weight byte.  The LDS holds a strip of
+//    KP floats of every sequence (KP = 4096 at B = 8: 128 KiB; 8192 at 4; 12288 at 2), so a
+//    phase whose rows are longer (W2's K = 11008 at B = 4 or 8) runs in K-passes: pass q stages
+//    x[b][q*KP .. q*KP + KP) of every sequence, then the streaming waves sweep those chunks of
+//    every row the block owns.  A slot is one 8-KiB row chunk (KC = 2048 floats), as in the
+//    batch-1 step, and its consume does B dot products with the strip (B ds_read_b128 per weight
+//    float4).
 //  * RMSNorm needs the whole row's sum of squares before any element is scaled, which a K-pass
 //    does not have; the norm is applied as (W (w * x)) * ss_b: the staging multiplies by the norm
 //    weight w[k], accumulates sum x^2 per sequence over the passes (fixed order), and the
@@ -47,6 +47,7 @@ constexpr int NBUF = 2;         // register slots in flight per streaming wave
 constexpr int PL = 8;           // wave-loads per slot (8 KiB)
 constexpr int KC = PL * 256;    // floats per row chunk = one K-pass
 constexpr int KC4 = KC / 4;     // float4 per chunk
+constexpr int SBU = 4;          // staging: (sequence, float4) units in flight per thread
 constexpr int kResid = 256;     // residual-stream slice per block and sequence (LDS)
 constexpr unsigned kSpinLimit = 1u << 18;
 constexpr unsigned kXcdSkew = 4;  // percent; odd blockIdx (XCDs 1,3,5,7) stream slower (persist.hip)
@@ -110,9 +111,22 @@ TL_DEVICE PDesc next_desc(const PStep& p, int kind, int l, unsigned tb) {
 // This block's share of a phase (wave-uniform): items [i0, i0 + ni), their rows, the passes.
 struct PGeo {
   int i0, ni;
-  int nrow;  // ni * rpi: the slots of every pass
-  int nch;   // K-passes (row chunks)
+  int nrow;  // ni * rpi
+  int nch;   // row chunks (KC floats each)
 };
+
+// Pass q of a phase whose rows have nch chunks, cpp chunks per pass: chunks [c0, c0 + npc).
+struct PPass {
+  int c0, npc;
+  int nslot;  // nrow * npc: slot s = chunk c0 + s % npc of row s / npc
+};
+TL_DEVICE PPass pass_of(const PGeo& g, int cpp, int q) {
+  PPass r;
+  r.c0 = q * cpp;
+  r.npc = g.nch - r.c0 < cpp ? g.nch - r.c0 : cpp;
+  r.nslot = g.nrow * r.npc;
+  return r;
+}
 
 __host__ __device__ inline unsigned part_weight(unsigned b) { return (b >> 1) * 200u + (b & 1u) * (100u + kXcdSkew); }
 
@@ -156,28 +170,40 @@ TL_DEVICE void load_slot(const PDesc& d, const PGeo& g, const PStep& p, int rl, 
   }
 }
 
-// B dot products of one row chunk with the staged strip xs [NB][KC4] (sequences >= B skipped):
-// row partial res[(rl * nch + c) * NB + b].  One weight float4 at a time against every
-// sequence (B LDS reads in flight: the slot buffers stay the only large register set).
+// NB dot products of one row chunk with the staged strip (chunk cc of the pass: xs [NB][KP4] at
+// cc * KC4): row partial res[(rl * nch + c) * NB + b].  NB is the exact batch (no run-time guards:
+// a branch around each read made the compiler wait for it singly).
 template <int NB>
-TL_DEVICE void consume_slot(int rl, int c, int nch, int B, int lane, const f4 (&buf)[PL], const f4* xs, float* res) {
+TL_DEVICE void consume_slot(int rl, int c, int cc, int nch, int KP4, int lane, const f4 (&buf)[PL], const f4* xs,
+                            float* res) {
   float a[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) a[b] = 0.f;
-#pragma unroll
-  for (int u = 0; u < PL; ++u) {
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-      if (b < B) a[b] = dot4(buf[u], xs[b * KC4 + u * 64 + lane], a[b]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
+  // the strip offset is laundered so the compiler cannot prove the reads loop-invariant across
+  // the slots of a pass (a pass of one chunk reads the same strip for every slot)
+  int xo = cc * KC4 + lane;
+  asm volatile("" : "+v"(xo));
+  const f4* xc = xs + xo;
+  // one sequence at a time: its 8 strip reads in flight, then its 32 FMAs
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    if (b < B) {
-      const float s = wave_sum_u(a[b]);
-      if (lane == 0) res[(rl * nch + c) * NB + b] = s;
-    }
+    f4 xv[PL];
+#pragma unroll
+    for (int u = 0; u < PL; ++u) xv[u] = xc[b * KP4 + u * 64];
+#pragma unroll
+    for (int u = 0; u < PL; ++u) a[b] = dot4(buf[u], xv[u], a[b]);
+    __builtin_amdgcn_sched_barrier(0);
   }
+  // lane b keeps sequence b's sum and ONE store writes them all (a store per sequence under
+  // lane == 0 let the compiler sink each sequence's FMAs into its branch, after every read, and
+  // hold 8 float4 per sequence live: spills from 6 sequences on)
+  float mine = 0.f;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const float sm = wave_sum_u(a[b]);
+    mine = lane == b ? sm : mine;
+  }
+  if (lane < NB) res[(rl * nch + c) * NB + lane] = mine;
 }
 
 // A wave's slots in pass c: its two prefetched rows (sw, sw + NSW), then rows dealt from the
@@ -189,90 +215,97 @@ TL_DEVICE int take_slot(unsigned* ctr, int lane) {
 }
 
 template <int NB>
-TL_DEVICE void run_pass(const PDesc& d, const PGeo& g, const PStep& p, int c, int sw, int lane, const f4* xs,
-                        float* res, f4 (&buf)[NBUF][PL], unsigned* ctr) {
+TL_DEVICE void run_pass(const PDesc& d, const PGeo& g, const PPass& q, const PStep& p, int sw, int lane,
+                        const f4* xs, float* res, f4 (&buf)[NBUF][PL], unsigned* ctr, unsigned long long* ts) {
+  const int KP4 = p.pad_floats >> 2;
   int sl[NBUF];
 #pragma unroll
   for (int i = 0; i < NBUF; ++i) sl[i] = sw + i * NSW;
-  while (sl[0] < g.nrow) {
+  bool first = true;
+  while (sl[0] < q.nslot) {
 #pragma unroll
     for (int i = 0; i < NBUF; ++i) {
-      if (sl[i] < g.nrow) consume_slot<NB>(sl[i], c, g.nch, p.B, lane, buf[i], xs, res);
+      if (sl[i] < q.nslot) {
+        const int rl = sl[i] / q.npc, cc = sl[i] - rl * q.npc;
+        consume_slot<NB>(rl, q.c0 + cc, cc, g.nch, KP4, lane, buf[i], xs, res);
+      }
+      if (i == 0 && ts && first && lane == 0) *ts = __builtin_amdgcn_s_memrealtime();  // first slot landed
+      first = false;
       __builtin_amdgcn_sched_barrier(0);
       sl[i] = take_slot(ctr, lane);
-      if (sl[i] < g.nrow) load_slot(d, g, p, sl[i], c, lane, buf[i]);
+      if (sl[i] < q.nslot) load_slot(d, g, p, sl[i] / q.npc, q.c0 + sl[i] % q.npc, lane, buf[i]);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
 }
 
-// Stage pass c of the phase input for every sequence into xs [NB][KC4], multiplied by the norm
-// weight when the phase has one; its squares go, per wave and sequence, to red[wave * NB + b]
-// (summed there, not carried: the staging runs while the slot buffers are live).  Input: the
-// previous phase's granules (a group of sequences in flight at once, re-polled until their tags
-// match), or — QKV at layer 0 — the tokens' embedding rows.  Thread t < 512 owns float4 column t.
-template <int NB>
-TL_DEVICE void stage_pass(const PDesc& d, const PStep& p, int c, f4* xs, const float* rmsw, float* red, int wave,
-                          int lane) {
-  const int t = threadIdx.x;
-  const bool act = t < KC4;
-  const int n4 = d.K >> 2;
-  const int k4 = c * KC4 + t;  // float4 index in the row
-  const bool live = act && k4 < n4;
-  f4 w = f4{1.f, 1.f, 1.f, 1.f};
-  if (d.rms && live) w = reinterpret_cast<const f4*>(rmsw)[k4];
-  constexpr int GS = NB < 2 ? NB : 2;  // sequences whose granules are in flight together
+// A pass's first NBUF slots of this wave (its prefetch).
+TL_DEVICE void prefetch_pass(const PDesc& d, const PGeo& g, const PPass& q, const PStep& p, int sw, int lane,
+                             f4 (&buf)[NBUF][PL]) {
 #pragma unroll
-  for (int b0 = 0; b0 < NB; b0 += GS) {
-    f4 v[GS];
-    if (d.gin) {
-      const auto r = rsrc_of(d.gin);
-      v4u a[GS], bb[GS];
-#pragma unroll
-      for (int j = 0; j < GS; ++j) {
-        const int b = b0 + j;
-        if (live && b < p.B) {
-          const unsigned off = (unsigned)(b * n4 + k4) * 32u;
-          a[j] = ld16_sc1(r, off);
-          bb[j] = ld16_sc1(r, off + 16u);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < GS; ++j) {
-        const int b = b0 + j;
-        v[j] = f4{0.f, 0.f, 0.f, 0.f};
-        if (live && b < p.B)
-          v[j] = gran4_ok(a[j], bb[j], d.tag_in) ? gran4_val(a[j], bb[j])
-                                                : gran_wait4(r, (unsigned)(b * n4 + k4) * 32u, d.tag_in, p.err);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < GS; ++j) {
-        const int b = b0 + j;
-        v[j] = live && b < p.B ? reinterpret_cast<const f4*>(p.emb + (long long)p.tok[b] * p.dim)[k4]
-                               : f4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < GS; ++j) {
-      const int b = b0 + j;
-      if (d.rms) {
-        float q = 0.f;
-        q = fmaf(v[j].x, v[j].x, q); q = fmaf(v[j].y, v[j].y, q);
-        q = fmaf(v[j].z, v[j].z, q); q = fmaf(v[j].w, v[j].w, q);
-        q = wave_sum_u(q);
-        if (lane == 0) red[wave * NB + b] = q;
-        v[j] = f4{__fmul_rn(w.x, v[j].x), __fmul_rn(w.y, v[j].y), __fmul_rn(w.z, v[j].z), __fmul_rn(w.w, v[j].w)};
-      }
-      if (act) xs[b * KC4 + t] = v[j];
-    }
+  for (int i = 0; i < NBUF; ++i) {
+    const int s = sw + i * NSW;
+    if (s < q.nslot) load_slot(d, g, p, s / q.npc, q.c0 + s % q.npc, lane, buf[i]);
   }
 }
 
-TL_DEVICE void preload_rms(const float* w, int dim, float* rmsw, int lane) {
-  const f4* s4 = reinterpret_cast<const f4*>(w);
-  f4* d4 = reinterpret_cast<f4*>(rmsw);
-  for (int j = lane; j < (dim >> 2); j += 64) d4[j] = s4[j];
+// Stage pass q (floats [q*KP, q*KP + KP) of the row) of every sequence into xs [NB][KP4],
+// multiplied by the norm weight when the phase has one (read from global memory: constants, in
+// L2); the squares go, per wave and sequence, to red[wave * NB + b].  Input: the previous
+// phase's granules (SBU (sequence, float4) units in flight per thread, re-polled until their
+// tags match), or — QKV at layer 0 — the tokens' embedding rows.  Unit u = t + k * PT covers
+// float4 u % KP4 of sequence u / KP4, so a wave reads 2 KiB of consecutive granules.
+template <int NB>
+TL_DEVICE void stage_pass(const PDesc& d, const PStep& p, int q, f4* xs, float* red, int wave, int lane) {
+  const int t = threadIdx.x;
+  const int KP4 = p.pad_floats >> 2;
+  const int n4 = d.K >> 2;
+  const int U = NB * KP4;
+  float sq[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) sq[b] = 0.f;
+  const auto r = rsrc_of(d.gin ? (const void*)d.gin : (const void*)p.emb);
+  for (int u0 = t; u0 < U; u0 += SBU * PT) {
+    v4u ga[SBU], gb[SBU];
+#pragma unroll
+    for (int k = 0; k < SBU; ++k) {
+      const int u = u0 + k * PT, b = u / KP4, k4 = q * KP4 + (u - b * KP4);
+      if (d.gin && u < U && k4 < n4) {
+        const unsigned off = (unsigned)(b * n4 + k4) * 32u;
+        ga[k] = ld16_sc1(r, off);
+        gb[k] = ld16_sc1(r, off + 16u);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < SBU; ++k) {
+      const int u = u0 + k * PT, b = u / KP4, j = u - b * KP4, k4 = q * KP4 + j;
+      if (u >= U) continue;
+      f4 v = f4{0.f, 0.f, 0.f, 0.f};
+      if (k4 < n4) {
+        if (d.gin)
+          v = gran4_ok(ga[k], gb[k], d.tag_in) ? gran4_val(ga[k], gb[k])
+                                               : gran_wait4(r, (unsigned)(b * n4 + k4) * 32u, d.tag_in, p.err);
+        else
+          v = reinterpret_cast<const f4*>(p.emb + (long long)p.tok[b] * p.dim)[k4];
+        if (d.rms) {
+          float s2 = 0.f;
+          s2 = fmaf(v.x, v.x, s2); s2 = fmaf(v.y, v.y, s2); s2 = fmaf(v.z, v.z, s2); s2 = fmaf(v.w, v.w, s2);
+#pragma unroll
+          for (int bb = 0; bb < NB; ++bb) sq[bb] += bb == b ? s2 : 0.f;
+          const f4 w = reinterpret_cast<const f4*>(d.rms)[k4];
+          v = f4{__fmul_rn(w.x, v.x), __fmul_rn(w.y, v.y), __fmul_rn(w.z, v.z), __fmul_rn(w.w, v.w)};
+        }
+      }
+      xs[b * KP4 + j] = v;
+    }
+  }
+  if (d.rms) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const float s2 = wave_sum_u(sq[b]);
+      if (lane == 0) red[wave * NB + b] = s2;
+    }
+  }
 }
 
 // Control wave: row values from the pass partials (chunks in order), the norm scale, the fused
@@ -285,9 +318,9 @@ TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const flo
   for (int b = 0; b < NB; ++b) best[b] = 0;
   // (item, sequence) pairs over the lanes: a block owns 16-130 items, so items alone would
   // leave most lanes idle on this hand-off's critical path
-  const int npair = g.ni * p.B;
+  const int npair = g.ni * NB;
   for (int j = lane; j < npair; j += 64) {
-    const int it = j / p.B, b = j - it * p.B;
+    const int it = j / NB, b = j - it * NB;
     const int item = g.i0 + it;
     float v[2] = {0.f, 0.f};
     for (int r = 0; r < d.rpi; ++r) {
@@ -338,7 +371,7 @@ TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const flo
         const unsigned long long other = __shfl_xor(bv, o, 64);
         bv = other > bv ? other : bv;
       }
-      if (lane == 0 && b < p.B) st8_sc1(p.bmax + (long long)blockIdx.x * NB + b, bv);
+      if (lane == 0 && b < NB) st8_sc1(p.bmax + (long long)blockIdx.x * NB + b, bv);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drained before the final arrival
   }
@@ -369,13 +402,23 @@ TL_DEVICE void grid_barrier(const PStep& p) {
   __syncthreads();
 }
 
+// Optional timeline (PStep::trace, [grid][phase][kTraceSlots], 100-MHz clock), control wave:
+// 0 phase start, 1 first pass staged, 2 last pass swept, 3 epilogue (or attention units) done,
+// 8 + q pass q swept (q < 8); streaming wave 1: 4 its first slot of pass 0 consumed.
+#define TRACE_B(k)                                                                              \
+  do {                                                                                          \
+    if (p.trace && lane == 0)                                                                   \
+      p.trace[((long long)blockIdx.x * nph + ph) * kTraceSlots + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
 // The phase sequence as one wave sees it.  ROLE0 = the control wave.  Both run the same
 // workgroup barriers: per GEMV phase and pass, one after the staging and one after the sweep.
 template <int HS, int NB, bool ROLE0>
-TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xres, float* red, float* rmsw,
-                      f4* xs, const uint64_t* etab, unsigned tb) {
+TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xres, float* red, f4* xs,
+                      const uint64_t* etab, unsigned tb) {
   const int G = gridDim.x;
   const int nph = 5 * p.L + 1;
+  const int cpp = p.pad_floats / KC;  // row chunks per K-pass
   float* ssum = red + PW * NB;                                   // [NB] this phase's sum of squares
   float* sscale = ssum + NB;                                     // [NB] its norm scales (epilogue)
   unsigned* ctr = reinterpret_cast<unsigned*>(sscale + NB);      // dynamic slot counter
@@ -384,25 +427,23 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
   if constexpr (ROLE0) {
     // this block's slice of every sequence's residual stream starts as its embedding row
     const PGeo gx = geo(make_desc(p, PK_WO, 0, tb));
-    for (int b = 0; b < p.B; ++b) {
+    for (int b = 0; b < NB; ++b) {
       const float* er = p.emb + (long long)p.tok[b] * p.dim + gx.i0;
       for (int it = lane; it < gx.ni; it += 64) xres[b * kResid + it] = er[it];
     }
-    preload_rms(p.rms_att, p.dim, rmsw, lane);
     if (lane < NB) ssum[lane] = 0.f;
     if (lane == 0) *ctr = 0u;
   } else {
     const PDesc d0 = make_desc(p, PK_QKV, 0, tb);
     const PGeo g0 = geo(d0);
-#pragma unroll
-    for (int i = 0; i < NBUF; ++i)
-      if (sw + i * NSW < g0.nrow) load_slot(d0, g0, p, sw + i * NSW, 0, lane, buf[i]);
+    prefetch_pass(d0, g0, pass_of(g0, cpp, 0), p, sw, lane, buf);
   }
-  __syncthreads();  // first norm weights preloaded, counters set
+  __syncthreads();  // counters set
 
   for (int ph = 0; ph < nph; ++ph) {
     const int l = ph / 5;
     const int kind = ph == nph - 1 ? PK_CLS : ph % 5;
+    if constexpr (ROLE0) TRACE_B(0);
     if (kind == PK_ATTN) {
       if constexpr (!ROLE0) {  // the slot buffers are empty here: say so, so they are not kept live
 #pragma unroll
@@ -421,57 +462,53 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
         aw.a.pos = p.pos; aw.a.out = p.xb; aw.a.part = p.part;
         aw.a.dim = p.dim; aw.a.kv_dim = p.kvd; aw.a.head_size = HS; aw.a.n_heads = p.H;
         aw.a.kv_mul = p.kv_mul; aw.a.seq_len = p.S; aw.a.nsplit = p.NS; aw.a.min_chunk = 16;
-        aw.cnt = p.tickets + (long long)l * p.B * p.H; aw.B = p.B; aw.NS = p.NS;
+        aw.cnt = p.tickets + (long long)l * NB * p.H; aw.B = NB; aw.NS = p.NS;
         aw.gqkv = p.gqkv; aw.gout = p.gxb;
         aw.etab = etab;
         aw.tag_in = tb + 5u * l + 1; aw.tag_out = tb + 5u * l + 2; aw.err = p.err;
-        const int units = p.B * p.H * p.NS;
+        const int units = NB * p.H * p.NS;
         for (int u = blockIdx.x + G * wave; u < units; u += G * PW) attn_unit<HS, 16, true>(aw, u, lane);
+        if constexpr (ROLE0) TRACE_B(3);
       }
       if constexpr (!ROLE0) {  // Wo's first slots stream in while its input is gathered
         const PDesc nd = make_desc(p, PK_WO, l, tb);
         const PGeo ng = geo(nd);
-#pragma unroll
-        for (int i = 0; i < NBUF; ++i)
-          if (sw + i * NSW < ng.nrow) load_slot(nd, ng, p, sw + i * NSW, 0, lane, buf[i]);
+        prefetch_pass(nd, ng, pass_of(ng, cpp, 0), p, sw, lane, buf);
       }
       continue;
     }
     const PDesc d = make_desc(p, kind, kind == PK_CLS ? p.L : l, tb);
     const PGeo g = geo(d);
-    for (int c = 0; c < g.nch; ++c) {
-      stage_pass<NB>(d, p, c, xs, rmsw, red, wave, lane);
+    const int npass = (g.nch + cpp - 1) / cpp;
+    for (int q = 0; q < npass; ++q) {
+      stage_pass<NB>(d, p, q, xs, red, wave, lane);
       __syncthreads();  // strip staged (and this pass's squares per wave in red)
       if constexpr (ROLE0) {
+        if (q == 0) TRACE_B(1);
         if (d.rms && lane < NB) {
           float s = ssum[lane];
           for (int w = 0; w < PW; ++w) s = __fadd_rn(s, red[w * NB + lane]);
           ssum[lane] = s;
         }
-        if (c == g.nch - 1) {  // the staging is done with this phase's norm weights: the next
-          if (kind == PK_QKV) preload_rms(p.rms_ffn + (long long)l * p.dim, p.dim, rmsw, lane);
-          if (kind == PK_UP)
-            preload_rms(l + 1 < p.L ? p.rms_att + (long long)(l + 1) * p.dim : p.rms_final, p.dim, rmsw, lane);
-        }
       } else {
-        run_pass<NB>(d, g, p, c, sw, lane, xs, res, buf, ctr);
+        run_pass<NB>(d, g, pass_of(g, cpp, q), p, sw, lane, xs, res, buf, ctr,
+                     p.trace && sw == 0 && q == 0 ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots + 4
+                                                  : nullptr);
       }
       __syncthreads();  // every slot of the pass reduced into res; the strip may be restaged
       if constexpr (ROLE0) {
+        if (q < 8) TRACE_B(8 + q);
+        if (q == npass - 1) TRACE_B(2);
         if (lane == 0) *ctr = 0u;  // the next pass's slot counter (used after its staging barrier)
       } else {
         // the next pass's (or the next GEMV phase's) first slots: their data streams in while the
         // strip is restaged, the hand-off is waited for and the epilogue runs
-        if (c + 1 < g.nch) {
-#pragma unroll
-          for (int i = 0; i < NBUF; ++i)
-            if (sw + i * NSW < g.nrow) load_slot(d, g, p, sw + i * NSW, c + 1, lane, buf[i]);
+        if (q + 1 < npass) {
+          prefetch_pass(d, g, pass_of(g, cpp, q + 1), p, sw, lane, buf);
         } else if (kind != PK_CLS && kind != PK_QKV) {  // (after QKV: once the attention units ran)
           const PDesc nd = next_desc(p, kind, l, tb);
           const PGeo ng = geo(nd);
-#pragma unroll
-          for (int i = 0; i < NBUF; ++i)
-            if (sw + i * NSW < ng.nrow) load_slot(nd, ng, p, sw + i * NSW, 0, lane, buf[i]);
+          prefetch_pass(nd, ng, pass_of(ng, cpp, 0), p, sw, lane, buf);
         }
       }
     }
@@ -483,6 +520,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
         ssum[lane] = 0.f;
       }
       epilogue<NB>(d, g, p, res, xres, sscale, lane, l, etab);
+      TRACE_B(3);
     }
   }
   grid_barrier(p);
@@ -490,7 +528,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
     if (blockIdx.x != 0) return;
     if (p.argmax) {
       // per sequence: argmax over the per-block winners + advance (src/llama.cpp:275-286)
-      for (int b = 0; b < p.B; ++b) {
+      for (int b = 0; b < NB; ++b) {
         unsigned long long best = 0;
         for (int i = lane; i < G; i += 64) {
           const unsigned long long k = ld8_sc1(p.bmax + (long long)i * NB + b);
@@ -517,10 +555,9 @@ template <int HS, int NB>
 __global__ void __launch_bounds__(PT) persistent_step_b_kernel(PStep p) {
   if (p.fault && blockIdx.x == 0) return;  // test hook: a missing block (every wait is bounded)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  f4* xs = reinterpret_cast<f4*>(smem);                      // NB * KC floats: the staged strip
-  float* xres = reinterpret_cast<float*>(xs + NB * KC4);    // NB * kResid: residual slices
-  float* rmsw = xres + NB * kResid;                         // dim: the norm weights
-  float* red = rmsw + p.dim;                                // PW * NB + 2 * NB + 4
+  f4* xs = reinterpret_cast<f4*>(smem);                          // NB * KP floats: the staged strip
+  float* xres = reinterpret_cast<float*>(xs + NB * (p.pad_floats >> 2));  // NB * kResid: residual slices
+  float* red = xres + NB * kResid;                              // PW * NB + 2 * NB + 4
   float* res = red + PW * NB + 2 * NB + 4;                  // n_res: row-chunk partials
   uint64_t* etab = reinterpret_cast<uint64_t*>(res + p.n_scr);  // the expf table (32 doubles' bits)
   {
@@ -530,25 +567,33 @@ __global__ void __launch_bounds__(PT) persistent_step_b_kernel(PStep p) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const unsigned tb = p.seq[0] << 12;  // tag base of this launch
-  if (wave == 0) phases<HS, NB, true>(p, wave, lane, res, xres, red, rmsw, xs, etab, tb);
-  else phases<HS, NB, false>(p, wave, lane, res, xres, red, rmsw, xs, etab, tb);
+  if (wave == 0) phases<HS, NB, true>(p, wave, lane, res, xres, red, xs, etab, tb);
+  else phases<HS, NB, false>(p, wave, lane, res, xres, red, xs, etab, tb);
 }
 
-static int nb_of(int B) { return B <= 2 ? 2 : B <= 4 ? 4 : 8; }
+static int nb_of(int B) { return B; }  // one instantiation per batch size: no run-time sequence guards
 
 static size_t lds_bytes(const PStep& p) {
   const int NB = nb_of(p.B);
-  return (size_t)NB * KC * 4 + (size_t)NB * kResid * 4 + (size_t)p.dim * 4 + (size_t)(PW * NB + 2 * NB + 4) * 4 +
+  return (size_t)NB * p.pad_floats * 4 + (size_t)NB * kResid * 4 + (size_t)(PW * NB + 2 * NB + 4) * 4 +
          (size_t)p.n_scr * 4 + 32 * 8;
 }
 
 template <int HS, int NB>
 static const void* kfn() { return (const void*)persistent_step_b_kernel<HS, NB>; }
-static const void* kernel_of(const PStep& p) {
-  const int NB = nb_of(p.B);
-  if (p.hs == 128) return NB == 2 ? kfn<128, 2>() : NB == 4 ? kfn<128, 4>() : kfn<128, 8>();
-  return NB == 2 ? kfn<64, 2>() : NB == 4 ? kfn<64, 4>() : kfn<64, 8>();
+template <int HS>
+static const void* kfn_b(int B) {
+  switch (B) {
+    case 2: return kfn<HS, 2>();
+    case 3: return kfn<HS, 3>();
+    case 4: return kfn<HS, 4>();
+    case 5: return kfn<HS, 5>();
+    case 6: return kfn<HS, 6>();
+    case 7: return kfn<HS, 7>();
+    default: return kfn<HS, 8>();
+  }
 }
+static const void* kernel_of(const PStep& p) { return p.hs == 128 ? kfn_b<128>(p.B) : kfn_b<64>(p.B); }
 
 }  // namespace pb
 
@@ -582,6 +627,16 @@ bool persistent_prepare_b(PStep& p, int ncu, const char** why) {
     nr = v > nr ? v : nr;
   p.n_scr = (nr + 3) & ~3;
   if ((long long)p.dim * (100 + kXcdSkew) / part_weight(ncu) + 2 > kResid) return fail("residual slice per block too large");
+  // the K-pass strip: as many whole chunks of every sequence as the LDS leaves room for, at most
+  // the longest row (one pass per phase where it fits)
+  {
+    const int kmax = ((p.dim > p.hid ? p.dim : p.hid) + KC - 1) / KC * KC;
+    p.pad_floats = 0;
+    const size_t rest = lds_bytes(p);
+    const long long room = (160 * 1024 - (long long)rest) / (NB * 4) / KC * KC;
+    if (room < KC) return fail("activations do not fit the LDS");
+    p.pad_floats = (int)(room < kmax ? room : kmax);
+  }
   if (lds_bytes(p) > 160 * 1024) return fail("activations do not fit the LDS");
   {  // more than 64 KiB of dynamic LDS (gfx950: 160 KiB per CU), once per device
     static std::mutex mu;
@@ -591,9 +646,10 @@ bool persistent_prepare_b(PStep& p, int ncu, const char** why) {
     std::lock_guard<std::mutex> lock(mu);
     const unsigned long long bit = dev < 64 ? 1ull << dev : 0ull;
     if (!bit || !(done & bit)) {
-      for (const void* f : {kfn<64, 2>(), kfn<64, 4>(), kfn<64, 8>(), kfn<128, 2>(), kfn<128, 4>(), kfn<128, 8>()})
-        if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-          return fail("cannot raise the dynamic LDS limit");
+      for (int b = 2; b <= 8; ++b)
+        for (const void* f : {kfn_b<64>(b), kfn_b<128>(b)})
+          if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+            return fail("cannot raise the dynamic LDS limit");
       done |= bit;
     }
   }

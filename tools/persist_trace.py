@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--pos", type=int, default=8, help="position of the traced step")
     ap.add_argument("--json", default="")
     ap.add_argument("--dtype", default="f32", choices=["f32", "int8"])
+    ap.add_argument("--batch", type=int, default=1, help="sequences (2..8: the batched step, persist_b.hip)")
     args = ap.parse_args()
     _pkg()
     from hip_llama_cpp_amd import thallama as tl
@@ -37,12 +38,13 @@ def main():
     model = tl.DeviceModel(c, 0, seed=7)
     if args.dtype == "int8":
         model = tl.DeviceModelQ8(c, 0, 64, from_model=model)
-    state = tl.DeviceState(c, 1)
+    B = args.batch
+    state = tl.DeviceState(c, B)
     dec = tl.Decoder(model, state)
     assert dec.persistent()
-    dec.greedy([1], [0], args.pos, want_tokens=False)
+    dec.greedy([1] * B, [0] * B, args.pos, want_tokens=False)
     dec.ptrace(True)
-    dec.greedy([1], [args.pos], 1, want_tokens=False)
+    dec.greedy([1] * B, [args.pos] * B, 1, want_tokens=False)
     t = dec.ptrace(False).astype(np.int64)
     L = cfg[2]
     nph = 5 * L + 1
@@ -55,6 +57,37 @@ def main():
     esz = 4 if args.dtype == "f32" else 1 + 4 / 64  # int8 + one fp32 scale per 64
     wbytes = {k: v * esz for k, v in {"qkv": dim * (dim + 2 * kvd), "attn": 0, "wo": dim * dim, "ffn_up": 2 * dim * hid,
                                        "ffn_down": dim * hid, "cls": dim * V}.items()}
+    if B > 1:  # the batched step (persist_b.hip): its own slots, see TRACE_B there
+        print(f"{args.model} B={B}: {G} blocks, step {t[:, -1, 3].max() - t[:, 0, 0].min():.1f} us")
+        print(f"{'kind':9s}{'phase':>8s}{'stage0':>8s}{'slot0':>8s}{'passes':>40s}{'epi':>7s}{'GB/s':>8s}")
+        out = {}
+        for kind, k in (("qkv", 0), ("attn", 1), ("wo", 2), ("ffn_up", 3), ("ffn_down", 4), ("cls", nph - 1)):
+            phs = [k] if kind == "cls" else list(range(k, nph - 1, 5))
+            phase = np.median([t[:, ph + 1, 0].max() - t[:, ph, 0].max() for ph in phs if ph + 1 < nph]) \
+                if kind != "cls" else float(t[:, -1, 3].max() - t[:, -1, 0].max())
+            if kind == "attn":
+                done = np.median([np.median(t[:, ph, 3] - t[:, ph, 0]) for ph in phs])
+                print(f"{kind:9s}{phase:8.2f}   units done (median) {done:.2f}")
+                out[kind] = {"phase": float(phase)}
+                continue
+            stage0 = np.median([np.median(t[:, ph, 1] - t[:, ph, 0]) for ph in phs])
+            slot0 = np.median([np.median(t[:, ph, 4] - t[:, ph, 1]) for ph in phs])
+            K = cfg[1] if kind == "ffn_down" else cfg[0]
+            nch = (K + 2047) // 2048
+            passes = []
+            for c in range(min(nch, 8)):
+                prev = 1 if c == 0 else 8 + c - 1
+                passes.append(float(np.median([np.median(t[:, ph, 8 + c] - t[:, ph, prev]) for ph in phs])))
+            epi = np.median([np.median(t[:, ph, 3] - t[:, ph, 2]) for ph in phs])
+            gbs = wbytes[kind] / (phase * 1e-6) / 1e9
+            print(f"{kind:9s}{phase:8.2f}{stage0:8.2f}{slot0:8.2f}{' '.join(f'{v:5.2f}' for v in passes):>40s}"
+                  f"{epi:7.2f}{gbs:8.0f}")
+            out[kind] = {"phase": float(phase), "stage0": float(stage0), "slot0": float(slot0), "passes": passes,
+                         "epilogue": float(epi), "GBps": float(gbs)}
+        if args.json:
+            with open(args.json, "w") as f:
+                json.dump(out, f, indent=1)
+        return
     rows = {}
     for ph in range(nph):
         kind = "cls" if ph == nph - 1 else KINDS[ph % 5]
