@@ -308,11 +308,28 @@ TL_DEVICE void stage_pass(const PDesc& d, const PStep& p, int q, f4* xs, float* 
   }
 }
 
+// Control wave, while the QKV rows stream: the RoPE (cos, sin) of every (item, sequence) pair of
+// this block into LDS (a table read inside the epilogue put an L2 round trip per 64 pairs on
+// the hand-off's critical path).
+template <int NB>
+TL_DEVICE void rope_preload(const PGeo& g, const PStep& p, float2* rcs, int lane) {
+  for (int j = lane; j < g.ni * NB; j += 64) {
+    const int it = j / NB, b = j - it * NB;
+    const int row = 2 * (g.i0 + it);
+    float2 cs = make_float2(1.f, 0.f);
+    if (row < p.dim + p.kvd) {
+      const int i = row < p.dim ? row : row - p.dim;
+      cs = p.rope[(long long)p.pos[b] * (p.hs >> 1) + ((i % p.hs) >> 1)];
+    }
+    rcs[j] = cs;
+  }
+}
+
 // Control wave: row values from the pass partials (chunks in order), the norm scale, the fused
 // epilogue, granule stores.  xres: this block's slice of every sequence's residual stream.
 template <int NB>
 TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const float* res, float* xres,
-                        const float* ss, int lane, int l, const uint64_t* etab) {
+                        const float* ss, int lane, int l, const uint64_t* etab, const float2* rcs) {
   unsigned long long best[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) best[b] = 0;
@@ -347,8 +364,7 @@ TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const flo
       const int pb = p.pos[b];
       float a0 = v[0], a1 = v[1];
       if (row < p.dim + p.kvd) {
-        const int i = row < p.dim ? row : row - p.dim;
-        const float2 cs = p.rope[(long long)pb * (p.hs >> 1) + ((i % p.hs) >> 1)];
+        const float2 cs = rcs[j];  // (loaded during the sweep: rope_preload)
         const float r0 = __fsub_rn(__fmul_rn(a0, cs.x), __fmul_rn(a1, cs.y));
         const float r1 = __fadd_rn(__fmul_rn(a0, cs.y), __fmul_rn(a1, cs.x));
         a0 = r0; a1 = r1;
@@ -415,7 +431,7 @@ TL_DEVICE void grid_barrier(const PStep& p) {
 // workgroup barriers: per GEMV phase and pass, one after the staging and one after the sweep.
 template <int HS, int NB, bool ROLE0>
 TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xres, float* red, f4* xs,
-                      const uint64_t* etab, unsigned tb) {
+                      const uint64_t* etab, float2* rcs, unsigned tb) {
   const int G = gridDim.x;
   const int nph = 5 * p.L + 1;
   const int cpp = p.pad_floats / KC;  // row chunks per K-pass
@@ -490,6 +506,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
           for (int w = 0; w < PW; ++w) s = __fadd_rn(s, red[w * NB + lane]);
           ssum[lane] = s;
         }
+        if (kind == PK_QKV && q == 0) rope_preload<NB>(g, p, rcs, lane);
       } else {
         run_pass<NB>(d, g, pass_of(g, cpp, q), p, sw, lane, xs, res, buf, ctr,
                      p.trace && sw == 0 && q == 0 ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots + 4
@@ -519,7 +536,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
         sscale[lane] = d.rms ? __fdiv_rn(1.0f, sqrtf(__fadd_rn(__fdiv_rn(ssum[lane], (float)d.K), 1e-5f))) : 1.f;
         ssum[lane] = 0.f;
       }
-      epilogue<NB>(d, g, p, res, xres, sscale, lane, l, etab);
+      epilogue<NB>(d, g, p, res, xres, sscale, lane, l, etab, rcs);
       TRACE_B(3);
     }
   }
@@ -560,6 +577,7 @@ __global__ void __launch_bounds__(PT) persistent_step_b_kernel(PStep p) {
   float* red = xres + NB * kResid;                              // PW * NB + 2 * NB + 4
   float* res = red + PW * NB + 2 * NB + 4;                  // n_res: row-chunk partials
   uint64_t* etab = reinterpret_cast<uint64_t*>(res + p.n_scr);  // the expf table (32 doubles' bits)
+  float2* rcs = reinterpret_cast<float2*>(etab + 32);          // [QKV items][NB] RoPE (cos, sin)
   {
     constexpr uint64_t tab[32] = TL_EXPF_TABLE;
     if (threadIdx.x < 32) etab[threadIdx.x] = tab[threadIdx.x];  // (read after the first barrier)
@@ -567,8 +585,13 @@ __global__ void __launch_bounds__(PT) persistent_step_b_kernel(PStep p) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const unsigned tb = p.seq[0] << 12;  // tag base of this launch
-  if (wave == 0) phases<HS, NB, true>(p, wave, lane, res, xres, red, xs, etab, tb);
-  else phases<HS, NB, false>(p, wave, lane, res, xres, red, xs, etab, tb);
+  if (wave == 0) {
+    // the control wave's epilogues are every other block's hand-off: first call on the issue slots
+    __builtin_amdgcn_s_setprio(2);
+    phases<HS, NB, true>(p, wave, lane, res, xres, red, xs, etab, rcs, tb);
+  } else {
+    phases<HS, NB, false>(p, wave, lane, res, xres, red, xs, etab, rcs, tb);
+  }
 }
 
 static int nb_of(int B) { return B; }  // one instantiation per batch size: no run-time sequence guards
@@ -576,7 +599,7 @@ static int nb_of(int B) { return B; }  // one instantiation per batch size: no r
 static size_t lds_bytes(const PStep& p) {
   const int NB = nb_of(p.B);
   return (size_t)NB * p.pad_floats * 4 + (size_t)NB * kResid * 4 + (size_t)(PW * NB + 2 * NB + 4) * 4 +
-         (size_t)p.n_scr * 4 + 32 * 8;
+         (size_t)p.n_scr * 4 + 32 * 8 + (size_t)p.n_sqa * 8;
 }
 
 template <int HS, int NB>
@@ -626,6 +649,7 @@ bool persistent_prepare_b(PStep& p, int ncu, const char** why) {
                 nres(p.hid, p.dim, 1), nres(p.dim, p.V, 1)})
     nr = v > nr ? v : nr;
   p.n_scr = (nr + 3) & ~3;
+  p.n_sqa = (int)(((long long)(p.dim + 2 * p.kvd) / 2 * (100 + kXcdSkew) / part_weight(ncu) + 2) * NB);  // RoPE pairs
   if ((long long)p.dim * (100 + kXcdSkew) / part_weight(ncu) + 2 > kResid) return fail("residual slice per block too large");
   // the K-pass strip: as many whole chunks of every sequence as the LDS leaves room for, at most
   // the longest row (one pass per phase where it fits)

@@ -72,10 +72,10 @@ def main():
                 continue
             stage0 = np.median([np.median(t[:, ph, 1] - t[:, ph, 0]) for ph in phs])
             slot0 = np.median([np.median(t[:, ph, 4] - t[:, ph, 1]) for ph in phs])
-            K = cfg[1] if kind == "ffn_down" else cfg[0]
-            nch = (K + 2047) // 2048
             passes = []
-            for c in range(min(nch, 8)):
+            for c in range(8):  # pass q's end is slot 8 + q (stamped only for the passes there were)
+                if not all((raw[:, ph, 8 + c] > raw[:, ph, 0]).all() for ph in phs):
+                    break
                 prev = 1 if c == 0 else 8 + c - 1
                 passes.append(float(np.median([np.median(t[:, ph, 8 + c] - t[:, ph, prev]) for ph in phs])))
             epi = np.median([np.median(t[:, ph, 3] - t[:, ph, 2]) for ph in phs])
