@@ -11,10 +11,10 @@ several threads without changing any row's summation order), same synthetic mode
 tests/golden/reference_long.json's llama2_7b case, which src/seq.cpp itself produced — checked
 here before anything is written, and again by tests/test_golden_2048.py.
 
-Recorded per step: the token, the top-2 margin, the digest of make_golden.py, and — for the
-drift curve of a GPU decode against this one — the float32 values at 72 logit indices (the
-step's top-8 ids, then 64 fixed ids).  Full float32 logits of steps 255, 1023 and 2047 go to the
-.npz.  Data only (inputs + outputs).  Run: python tests/golden/make_golden_2048.py [threads]
+Recorded per step: the token, the top-2 margin and ids; the digest of make_golden.py at six
+steps; and — for the drift curve of a GPU decode against this one — the float32 values at 72 logit
+indices (the step's top-8 ids, then 64 fixed ids) in the .npz, with the full float32 logits of
+steps 255, 1023 and 2047.  Data only (inputs + outputs).  Run: python tests/golden/make_golden_2048.py [threads]
 (~1-2 h on 7 threads, ~32 GB RAM).  Progress is saved every 64 steps; a rerun resumes.
 """
 import json
@@ -91,10 +91,15 @@ def main():
            "reference": "oracle/oracle.c forward (bit-exact src/seq.cpp:53-183 restatement), greedy = sample_argmax "
                         "(src/llama.cpp:275-286); first 256 steps equal reference_long.json (src/seq.cpp itself)",
            "config": list(CFG), "shared": 0, "seed": SEED, "start_token": 1, "start_pos": 0, "steps": STEPS,
-           "fixed_probe_ids": FIXED_IDS, **st}
+           "fixed_probe_ids": FIXED_IDS, "tokens": st["tokens"], "margins": st["margins"],
+           "top2": [ids[:2] for ids in st["probe_ids"]],
+           "digests_at": {str(k): st["digests"][k] for k in (0, 255, 511, 1023, 1535, 2047)},
+           "probes": "reference_2048_logits.npz: probe_ids [2048][72] (the step's top-8 ids, then fixed_probe_ids) "
+                     "and probe_vals (float32 logits there)"}
     with open(OUT_JSON, "w") as f:
         json.dump(out, f, separators=(",", ":"))
-    np.savez(OUT_NPZ, **full)
+    np.savez(OUT_NPZ, probe_ids=np.array(st["probe_ids"], np.int32), probe_vals=np.array(st["probe_vals"], np.float32),
+             **full)
     os.remove(PART)
     os.remove(OUT_NPZ + ".part.npz")
 
