@@ -256,7 +256,8 @@ TL_DEVICE void prefetch_pass(const PDesc& d, const PGeo& g, const PPass& q, cons
 // tags match), or — QKV at layer 0 — the tokens' embedding rows.  Unit u = t + k * PT covers
 // float4 u % KP4 of sequence u / KP4, so a wave reads 2 KiB of consecutive granules.
 template <int NB>
-TL_DEVICE void stage_pass(const PDesc& d, const PStep& p, int q, f4* xs, float* red, int wave, int lane) {
+TL_DEVICE void stage_pass(const PDesc& d, const PStep& p, int q, f4* xs, float* red, int wave, int lane,
+                          unsigned long long* ts) {
   const int t = threadIdx.x;
   const int KP4 = p.pad_floats >> 2;
   const int n4 = d.K >> 2;
@@ -298,7 +299,9 @@ TL_DEVICE void stage_pass(const PDesc& d, const PStep& p, int q, f4* xs, float* 
       }
       xs[b * KP4 + j] = v;
     }
+    if (ts && lane == 0 && u0 == t) ts[0] = __builtin_amdgcn_s_memrealtime();  // first batch in
   }
+  if (ts && lane == 0) ts[1] = __builtin_amdgcn_s_memrealtime();  // swept
   if (d.rms) {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -329,14 +332,15 @@ TL_DEVICE void rope_preload(const PGeo& g, const PStep& p, float2* rcs, int lane
 // epilogue, granule stores.  xres: this block's slice of every sequence's residual stream.
 template <int NB>
 TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const float* res, float* xres,
-                        const float* ss, int lane, int l, const uint64_t* etab, const float2* rcs) {
+                        const float* ss, int wave, int lane, int l, const uint64_t* etab, const float2* rcs,
+                        unsigned long long* cbest) {
   unsigned long long best[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) best[b] = 0;
   // (item, sequence) pairs over the lanes: a block owns 16-130 items, so items alone would
   // leave most lanes idle on this hand-off's critical path
   const int npair = g.ni * NB;
-  for (int j = lane; j < npair; j += 64) {
+  for (int j = wave * 64 + lane; j < npair; j += PW * 64) {
     const int it = j / NB, b = j - it * NB;
     const int item = g.i0 + it;
     float v[2] = {0.f, 0.f};
@@ -387,9 +391,8 @@ TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const flo
         const unsigned long long other = __shfl_xor(bv, o, 64);
         bv = other > bv ? other : bv;
       }
-      if (lane == 0 && b < NB) st8_sc1(p.bmax + (long long)blockIdx.x * NB + b, bv);
+      if (lane == 0) cbest[wave * NB + b] = bv;  // (reduced over the waves before the final barrier)
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drained before the final arrival
   }
 }
 
@@ -420,7 +423,8 @@ TL_DEVICE void grid_barrier(const PStep& p) {
 
 // Optional timeline (PStep::trace, [grid][phase][kTraceSlots], 100-MHz clock), control wave:
 // 0 phase start, 1 first pass staged, 2 last pass swept, 3 epilogue (or attention units) done,
-// 8 + q pass q swept (q < 8); streaming wave 1: 4 its first slot of pass 0 consumed.
+// 8 + q pass q swept (q < 6), 5 / 6 pass 0's first staging batch in / its sweep done; streaming
+// wave 1: 4 its first slot of pass 0 consumed, 14 / 15 its first staging batch in / sweep done.
 #define TRACE_B(k)                                                                              \
   do {                                                                                          \
     if (p.trace && lane == 0)                                                                   \
@@ -431,7 +435,7 @@ TL_DEVICE void grid_barrier(const PStep& p) {
 // workgroup barriers: per GEMV phase and pass, one after the staging and one after the sweep.
 template <int HS, int NB, bool ROLE0>
 TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xres, float* red, f4* xs,
-                      const uint64_t* etab, float2* rcs, unsigned tb) {
+                      const uint64_t* etab, float2* rcs, unsigned long long* cbest, unsigned tb) {
   const int G = gridDim.x;
   const int nph = 5 * p.L + 1;
   const int cpp = p.pad_floats / KC;  // row chunks per K-pass
@@ -497,7 +501,10 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
     const PGeo g = geo(d);
     const int npass = (g.nch + cpp - 1) / cpp;
     for (int q = 0; q < npass; ++q) {
-      stage_pass<NB>(d, p, q, xs, red, wave, lane);
+      stage_pass<NB>(d, p, q, xs, red, wave, lane,
+                     p.trace && q == 0 && (wave == 0 || wave == 1)
+                         ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots + (wave == 0 ? 5 : 14)
+                         : nullptr);
       __syncthreads();  // strip staged (and this pass's squares per wave in red)
       if constexpr (ROLE0) {
         if (q == 0) TRACE_B(1);
@@ -507,6 +514,12 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
           ssum[lane] = s;
         }
         if (kind == PK_QKV && q == 0) rope_preload<NB>(g, p, rcs, lane);
+        if (q == npass - 1 && lane < NB) {
+          // reference rmsnorm scale (src/seq.cpp:3-16): 1 / sqrtf(sum / size + 1e-5f), for every
+          // wave's epilogue share (after the pass-end barrier)
+          sscale[lane] = d.rms ? __fdiv_rn(1.0f, sqrtf(__fadd_rn(__fdiv_rn(ssum[lane], (float)d.K), 1e-5f))) : 1.f;
+          ssum[lane] = 0.f;
+        }
       } else {
         run_pass<NB>(d, g, pass_of(g, cpp, q), p, sw, lane, xs, res, buf, ctr,
                      p.trace && sw == 0 && q == 0 ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots + 4
@@ -514,7 +527,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
       }
       __syncthreads();  // every slot of the pass reduced into res; the strip may be restaged
       if constexpr (ROLE0) {
-        if (q < 8) TRACE_B(8 + q);
+        if (q < 6) TRACE_B(8 + q);
         if (q == npass - 1) TRACE_B(2);
         if (lane == 0) *ctr = 0u;  // the next pass's slot counter (used after its staging barrier)
       } else {
@@ -529,16 +542,23 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
         }
       }
     }
-    if constexpr (ROLE0) {
-      if (lane < NB) {
-        // reference rmsnorm scale (src/seq.cpp:3-16): 1 / sqrtf(sum / size + 1e-5f); kept in LDS
-        // because the epilogue indexes it by a run-time sequence (a register array would go to scratch)
-        sscale[lane] = d.rms ? __fdiv_rn(1.0f, sqrtf(__fadd_rn(__fdiv_rn(ssum[lane], (float)d.K), 1e-5f))) : 1.f;
-        ssum[lane] = 0.f;
+    // every wave takes a share of the (item, sequence) pairs (the control wave alone spent ~0.5 us
+    // per 64 pairs on this hand-off's critical path); the streaming waves' next slots are in flight
+    epilogue<NB>(d, g, p, res, xres, sscale, wave, lane, l, etab, rcs, cbest);
+    if constexpr (ROLE0) TRACE_B(3);
+  }
+  __syncthreads();  // every wave's classifier winners in cbest
+  if constexpr (ROLE0) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      unsigned long long bv = lane < PW ? cbest[lane * NB + b] : 0ull;
+      for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long other = __shfl_xor(bv, o, 64);
+        bv = other > bv ? other : bv;
       }
-      epilogue<NB>(d, g, p, res, xres, sscale, lane, l, etab, rcs);
-      TRACE_B(3);
+      if (lane == 0) st8_sc1(p.bmax + (long long)blockIdx.x * NB + b, bv);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drained before the final arrival
   }
   grid_barrier(p);
   if constexpr (ROLE0) {
@@ -577,7 +597,8 @@ __global__ void __launch_bounds__(PT) persistent_step_b_kernel(PStep p) {
   float* red = xres + NB * kResid;                              // PW * NB + 2 * NB + 4
   float* res = red + PW * NB + 2 * NB + 4;                  // n_res: row-chunk partials
   uint64_t* etab = reinterpret_cast<uint64_t*>(res + p.n_scr);  // the expf table (32 doubles' bits)
-  float2* rcs = reinterpret_cast<float2*>(etab + 32);          // [QKV items][NB] RoPE (cos, sin)
+  unsigned long long* cbest = reinterpret_cast<unsigned long long*>(etab + 32);  // [PW][NB] per-wave winners
+  float2* rcs = reinterpret_cast<float2*>(cbest + PW * NB);    // [QKV items][NB] RoPE (cos, sin)
   {
     constexpr uint64_t tab[32] = TL_EXPF_TABLE;
     if (threadIdx.x < 32) etab[threadIdx.x] = tab[threadIdx.x];  // (read after the first barrier)
@@ -588,9 +609,9 @@ __global__ void __launch_bounds__(PT) persistent_step_b_kernel(PStep p) {
   if (wave == 0) {
     // the control wave's epilogues are every other block's hand-off: first call on the issue slots
     __builtin_amdgcn_s_setprio(2);
-    phases<HS, NB, true>(p, wave, lane, res, xres, red, xs, etab, rcs, tb);
+    phases<HS, NB, true>(p, wave, lane, res, xres, red, xs, etab, rcs, cbest, tb);
   } else {
-    phases<HS, NB, false>(p, wave, lane, res, xres, red, xs, etab, rcs, tb);
+    phases<HS, NB, false>(p, wave, lane, res, xres, red, xs, etab, rcs, cbest, tb);
   }
 }
 
@@ -599,7 +620,7 @@ static int nb_of(int B) { return B; }  // one instantiation per batch size: no r
 static size_t lds_bytes(const PStep& p) {
   const int NB = nb_of(p.B);
   return (size_t)NB * p.pad_floats * 4 + (size_t)NB * kResid * 4 + (size_t)(PW * NB + 2 * NB + 4) * 4 +
-         (size_t)p.n_scr * 4 + 32 * 8 + (size_t)p.n_sqa * 8;
+         (size_t)p.n_scr * 4 + 32 * 8 + (size_t)PW * NB * 8 + (size_t)p.n_sqa * 8;
 }
 
 template <int HS, int NB>

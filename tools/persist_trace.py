@@ -73,12 +73,17 @@ def main():
             stage0 = np.median([np.median(t[:, ph, 1] - t[:, ph, 0]) for ph in phs])
             slot0 = np.median([np.median(t[:, ph, 4] - t[:, ph, 1]) for ph in phs])
             passes = []
-            for c in range(8):  # pass q's end is slot 8 + q (stamped only for the passes there were)
+            for c in range(6):  # pass q's end is slot 8 + q (stamped only for the passes there were)
                 if not all((raw[:, ph, 8 + c] > raw[:, ph, 0]).all() for ph in phs):
                     break
                 prev = 1 if c == 0 else 8 + c - 1
                 passes.append(float(np.median([np.median(t[:, ph, 8 + c] - t[:, ph, prev]) for ph in phs])))
             epi = np.median([np.median(t[:, ph, 3] - t[:, ph, 2]) for ph in phs])
+            med = lambda a, b: float(np.median([np.median(t[:, ph, a] - t[:, ph, b]) for ph in phs]))  # noqa: E731
+            # staging of pass 0, from the phase start: control wave first batch in / swept, streaming
+            # wave 1 first batch in / swept
+            stg = [med(5, 0), med(6, 0), med(14, 0), med(15, 0)]
+            print(f"{'':9s} staging c.first {stg[0]:.2f} c.swept {stg[1]:.2f}  s.first {stg[2]:.2f} s.swept {stg[3]:.2f}")
             gbs = wbytes[kind] / (phase * 1e-6) / 1e9
             print(f"{kind:9s}{phase:8.2f}{stage0:8.2f}{slot0:8.2f}{' '.join(f'{v:5.2f}' for v in passes):>40s}"
                   f"{epi:7.2f}{gbs:8.0f}")
