@@ -243,12 +243,26 @@ static size_t granule_count(const thallama_decoder* d) {
 }
 
 // The batched persistent step (2..8 sequences, fp32): on unless THALLAMA_BATCH_PERSIST=0.
+// The batched persistent step (persist_b.hip) is prepared for 2..8 sequences unless
+// THALLAMA_BATCH_PERSIST=0, and taken BY DEFAULT for up to batch_persist_default_max() of them
+// (THALLAMA_OPT_PERSISTENT=1 selects it for the rest).  7B fp32 ms/step, persistent vs
+// multi-launch (profiles/r03/batch_persist_ab.json): B=2 4.69 vs 5.30, B=3 4.94 vs 7.04, B=4 5.21
+// vs 5.35, B=6 5.90 vs 5.59, B=8 6.57 vs 5.63 — past 4 sequences the all-gather hand-off of every
+// phase's input to every CU (B x K x 8 B of granules per CU per phase, 1.5 MB per layer at B=8)
+// costs more than the launches it saves; the matrix-core multi-launch kernels read K-split slices.
 static bool batch_persist_enabled() {
   static const bool on = [] {
     const char* e = getenv("THALLAMA_BATCH_PERSIST");
     return !(e && e[0] == '0');
   }();
   return on;
+}
+static int batch_persist_default_max() {
+  static const int v = [] {
+    const char* e = getenv("THALLAMA_BATCH_PERSIST");
+    return e && e[0] >= '1' && e[0] <= '9' ? atoi(e) : 4;
+  }();
+  return v;
 }
 
 extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg, const TransformerWeights* w,
@@ -337,6 +351,7 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
       d->pok = tl::persistent_prepare(ps, d->ncu, &why);
     } else if (batch <= 8 && batch_persist_enabled()) {
       d->pok = tl::persistent_prepare_b(ps, d->ncu, &why);
+      d->persist = batch <= batch_persist_default_max();
     } else {
       why = batch > 8 ? "batch > 8" : "THALLAMA_BATCH_PERSIST=0";
     }

@@ -32,9 +32,11 @@ enum {
   THALLAMA_OPT_ATTN_SPLITS = 2,  /* key splits per (head, seq); 0 = auto */
   THALLAMA_OPT_USE_GRAPH = 3,    /* 0/1: replay greedy steps from a captured hipGraph */
   THALLAMA_OPT_PROFILE = 4,      /* 0/1: HIP events around every kernel class (eager only) */
-  THALLAMA_OPT_PERSISTENT = 5,   /* 0/1: whole step as ONE persistent launch (batch 1, fp32,
-                                    head size 64/128; default 1 where supported).  Profiled
-                                    as the single class THALLAMA_K_STEP. */
+  THALLAMA_OPT_PERSISTENT = 5,   /* 0/1: whole step as ONE persistent launch (fp32 batch 1..8,
+                                    int8 batch 1; head size 64/128).  Default 1 where supported,
+                                    except fp32 batch 5..8 (default 0: slower than multi-launch
+                                    there; env THALLAMA_BATCH_PERSIST=N moves the bound, 0 never
+                                    prepares it).  Profiled as the single class THALLAMA_K_STEP. */
   THALLAMA_OPT_PERSIST_FAULT = 6,  /* test hook: the next persistent launch runs without its
                                     block 0 (as if the grid were not co-resident): its waits
                                     give up, the call disables the path and re-runs on the

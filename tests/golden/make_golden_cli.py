@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Generate tests/golden/cli_gen_in_128_greedy.json: BASELINE.json configs[0] as a fixture — the
-`-m test` output file for the first N prompts of the reference's assets/in/gen_in_128.txt (copied
+`-m test` output file for all 128 prompts of the reference's assets/in/gen_in_128.txt (copied
 verbatim to tests/golden/gen_in_128.txt) on a stories110M-shaped synthetic model, decoded
 greedily (`-g 1`), produced by the pinned CPU path:
   * forward: oracle/oracle.c, bit-identical to the reference's src/seq.cpp (tests/test_oracle.py);
@@ -10,7 +10,7 @@ greedily (`-g 1`), produced by the pinned CPU path:
     :891-1083 (test_data_parallelism: prompt tokens forced, then one token per step until
     BOS/EOS or seq_len, one "\\n" appended per request, another per line when written).
 The model is written as a v0 model.bin from the synthetic generator (config, seed below), so the
-GPU test rebuilds the identical file.  Run: python tests/golden/make_golden_cli.py  (~2 min, 8 cores)
+GPU test rebuilds the identical file.  Run: python tests/golden/make_golden_cli.py  (~15-20 min, 8 cores)
 """
 import json
 import multiprocessing as mp
@@ -27,7 +27,7 @@ sys.path.insert(0, os.path.join(REPO, "hip_llama.cpp_amd"))
 CFG = (768, 2048, 12, 12, 12, 32000, 1024)  # stories110M shape
 SHARED = 0  # an unshared classifier: a random-init shared one makes every greedy continuation repeat its last token
 SEED = 110
-N_PROMPTS = 16
+N_PROMPTS = 128
 PROMPTS_FILE = os.path.join(HERE, "gen_in_128.txt")
 TOK = os.path.join(HERE, "tokenizer.bin")
 OUT = os.path.join(HERE, "cli_gen_in_128_greedy.json")
@@ -73,7 +73,8 @@ def main():
            "prompts_file": "tests/golden/gen_in_128.txt (= reference assets/in/gen_in_128.txt)",
            "n_prompts": len(ps), "batch_independent": True,
            "output_file": body.decode("latin-1"), "total_achieved_tokens": sum(r[2] for r in res),
-           "generated_tokens": [r[3] for r in res]}
+           "generated_tokens": [r[3] for r in res],
+           "outputs": [r[1].decode("latin-1") for r in res], "achieved_tokens": [r[2] for r in res]}
     with open(OUT, "w") as f:
         json.dump(out, f)
     print(f"{len(ps)} prompts, {out['total_achieved_tokens']} tokens", file=sys.stderr)

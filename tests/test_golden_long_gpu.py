@@ -57,6 +57,8 @@ def test_fp32_256_step_greedy_equals_reference(gpu, name, path):
     multi = path.endswith("multilaunch")
     if multi:
         dec.set(gpu.OPT_PERSISTENT, 0)
+    if B == 8 and not multi:
+        dec.set(gpu.OPT_PERSISTENT, 1)  # 5..8 sequences: opt-in (multi-launch is the default there)
     assert dec.persistent() == (not multi)  # batch 4 / 8: the batched persistent step (persist_b.hip)
     n = case["steps"]
     got = dec.greedy([case["start_token"]] * B, [case["start_pos"]] * B, n)

@@ -37,6 +37,13 @@ def test_selection(gpu):
     # 2..8 sequences: the batched persistent step (persist_b.hip, tests/test_persist_b_gpu.py)
     _, _, _, dec = decoder(gpu, SMALL, 0, 1, 1, batch=2)
     assert dec.persistent()
+    # 5..8: prepared, but multi-launch unless asked for (forward.hip batch_persist_default_max)
+    c = gpu.Config.make(*SMALL)
+    model, state = gpu.DeviceModel(c, 0, seed=0), gpu.DeviceState(c, 8)
+    dec = gpu.Decoder(model, state)
+    assert not dec.persistent()
+    dec.set(gpu.OPT_PERSISTENT, 1)
+    assert dec.persistent()
     _, _, _, dec = decoder(gpu, SMALL, 0, 1, 1, batch=9)
     assert not dec.persistent()
 
