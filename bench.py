@@ -345,8 +345,12 @@ def main(argv=None):
                     "bytes_per_launch": step_bytes_p, "avg_us": round(stp["avg_us"], 2),
                     "positions": f"0..{P - 1}"}
         elif ffn:
-            mfma = B >= 4
-            kname = ("gemv_q8" if q8 else "gemv") + ("_mfma" if mfma else "") + "_kernel"
+            # the W1/W3 kernel the launcher picked for B sequences (gemv_launch.hpp launch_mode):
+            # the first of these the PMC pass saw
+            pre = "gemv_q8" if q8 else "gemv"
+            cands = [f"{pre}_rr_kernel", f"{pre}_mfma_kernel", f"{pre}_kernel"] if B >= 4 else [f"{pre}_kernel"]
+            seen = [c for c in cands if any(k.startswith(f"void tl::{c}<2") for k in pmc.get("kernels", {}))]
+            kname = seen[0] if seen else (f"{pre}_mfma_kernel" if B > 4 else cands[0])
             roof = {"bound": "hbm", "achieved": round(ffn["GBps"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ffn["GBps"] / HBM_PEAK_GBS, 4),
                     "traffic": traffic_of(f"void tl::{kname}<2") if pmc else None,

@@ -35,6 +35,7 @@ TL_DEVICE void split_range(int T, int nsplit, int min_chunk, int s, int& t0, int
 // LPK = lanes per key row = hs/4.
 template <int LPK>
 __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p) {
+  keep_implicit_args();  // common.hpp: rocprofv3 --pmc needs the hidden kernargs
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* red = reinterpret_cast<float*>(smem);  // 16
   float* sc = red + 16;                         // scores for this split (<= seq_len)
@@ -455,6 +456,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
 // Stand-alone launch: one 64-thread block per unit.
 template <int HS, int CH>
 __global__ void __launch_bounds__(64) attn_wave_kernel(AttnWaveParams w) {
+  keep_implicit_args();  // common.hpp: rocprofv3 --pmc needs the hidden kernargs
   attn_unit<HS, CH>(w, blockIdx.x, threadIdx.x);
 }
 
@@ -636,7 +638,9 @@ TL_DEVICE void attn_unit_split(const AttnWaveParams& w, int h, int c, int NG, fl
 }
 
 // out[b][h*hs + i] = sum_s o_s[i] e^{m_s-M} / sum_s l_s e^{m_s-M}
-static __global__ void __launch_bounds__(256) attn_combine_kernel(AttnParams p) {
+template <int kUnused = 0>
+__global__ void __launch_bounds__(256) attn_combine_kernel(AttnParams p) {
+  keep_implicit_args();  // common.hpp: rocprofv3 --pmc needs the hidden kernargs
   const int h = blockIdx.x, b = blockIdx.y;
   const int hs = p.head_size;
   const int T = p.pos[b] + 1;

@@ -191,6 +191,11 @@ TL_DEVICE unsigned long long ld8_sc1(const unsigned long long* p) {
 TL_DEVICE void st8_sc1(unsigned long long* p, unsigned long long v) {
   __hip_atomic_store(as_g64(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Keeps the hidden (implicit) kernel arguments in a kernel's kernarg segment.  A kernel that
+// never reads them gets a segment of its explicit arguments only (gemv_mfma_kernel: 344 B instead
+// of 600), and rocprofv3's counter-collection dispatch hook then faults on the host reading past
+// it (SIGSEGV at a page boundary inside hipLaunchKernel, profiles/r03/pmc_sigsegv_diagnosis.md).
+TL_DEVICE void keep_implicit_args() { asm volatile("" ::"s"(__builtin_amdgcn_implicitarg_ptr())); }
 // Buffer resource over [base, base + 2 GiB); `base` must be wave-uniform.
 TL_DEVICE __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7ffffff0, 0x00020000);

@@ -55,6 +55,7 @@ extern "C" const char* thallama_last_error(void) { return g_last_error.c_str(); 
 // (value, index) reduction that keeps the lower index on ties.
 __global__ void __launch_bounds__(1024) k_argmax_advance(const float* logits, int V, int* tok, int* pos,
                                                          int* out, int cap) {
+  tl::keep_implicit_args();  // common.hpp: rocprofv3 --pmc needs the hidden kernargs
   __shared__ unsigned long long red[16];
   const int b = blockIdx.x;
   const float* l = logits + (long long)b * V;
@@ -600,7 +601,7 @@ static int enqueue_step(thallama_decoder* d) {
       }
       TL_TRY(hipGetLastError());
       if (d->nsplit > 1) {
-        hipLaunchKernelGGL(tl::attn_combine_kernel, dim3(d->H, d->B), dim3(128), 0, d->stream, a);
+        hipLaunchKernelGGL(tl::attn_combine_kernel<0>, dim3(d->H, d->B), dim3(128), 0, d->stream, a);
         TL_TRY(hipGetLastError());
       }
       }

@@ -374,6 +374,7 @@ __global__ void __launch_bounds__(WAVES * 64) gemv_kernel(GemvParams p, int kc_m
 // pointers): one wave per (row, sequence), scalar loads.  Same epilogues.
 template <int MODE>
 __global__ void __launch_bounds__(256) gemv_generic_kernel(GemvParams p) {
+  keep_implicit_args();
   __shared__ float red[16];
   (void)red;
   constexpr int RPI = RowsPerItem<MODE>::v;

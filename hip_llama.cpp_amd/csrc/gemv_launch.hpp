@@ -156,7 +156,7 @@ inline hipError_t launch_mode(const GemvParams& p0, hipStream_t s, const GemvCfg
       // the scratch rows first; otherwise the kernel applies the norm itself
       if (p.tok || (p.rms_w && !p.ssq_in)) {
         p.ssq_in = nullptr;
-        hipLaunchKernelGGL(gemv_prenorm_kernel, dim3(p.nb), dim3(256), 0, s, p);
+        hipLaunchKernelGGL(gemv_prenorm_kernel<0>, dim3(p.nb), dim3(256), 0, s, p);
         p.x = p.xn;
         p.x_stride = p.K;
         p.rms_w = nullptr;

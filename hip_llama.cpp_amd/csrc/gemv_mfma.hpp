@@ -73,7 +73,8 @@ TL_DEVICE void epi_one(const GemvParams& p, int item, int b, float v0, float v1)
 
 // xn[b] = rms_w * (ss_b * x_b) (or x_b itself without a norm); x_b is the embedding row
 // tok[b] when tok is set, and then also copied to x_out (the residual stream).
-static __global__ void __launch_bounds__(256) gemv_prenorm_kernel(GemvParams p) {
+template <int kUnused = 0>
+__global__ void __launch_bounds__(256) gemv_prenorm_kernel(GemvParams p) {
   __shared__ float red[16];
   const int b = blockIdx.x;
   const int n4 = p.K >> 2;
@@ -114,6 +115,7 @@ static __global__ void __launch_bounds__(256) gemv_prenorm_kernel(GemvParams p) 
 // address and multiply zero activations, so no load is predicated.
 template <int MODE, bool NT, int XI>
 __global__ void __launch_bounds__(kMfmaWaves * 64) gemv_mfma_kernel(GemvParams p) {
+  keep_implicit_args();
   constexpr int W = kMfmaWaves;
   constexpr bool TWO = MODE == GM_SWIGLU;
   constexpr int NR = TWO ? 2 : 1;      // weight tiles per group; tile NR is the activations

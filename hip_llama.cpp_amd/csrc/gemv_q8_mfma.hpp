@@ -21,6 +21,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 template <int MODE, bool NT>
 __global__ void __launch_bounds__(kMfmaWaves * 64) gemv_q8_mfma_kernel(GemvParams p) {
+  keep_implicit_args();  // common.hpp
   constexpr int W = kMfmaWaves;
   constexpr bool TWO = MODE == GM_SWIGLU;
   constexpr int NR = TWO ? 2 : 1;  // weight tiles per run; tile NR is the activation codes

@@ -3,7 +3,7 @@
 
     python tools/rocprof_summary.py stats <results.db> <out.csv>
         kernel, calls, total_us, avg_us, percent  (the top_kernels view of --kernel-trace --stats)
-    python tools/rocprof_summary.py pmc <fetch_results.db> <write_results.db> <out.json> [note]
+    python tools/rocprof_summary.py pmc <fetch_results.db> <write_results.db> <out.json> [note] [model] [batch]
         per-kernel launch averages of FETCH_SIZE / WRITE_SIZE (separate --pmc passes) and
         traffic_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (gfx950: FETCH_SIZE counts half of
         the bytes of wide coalesced streaming reads, MI355X_MICROARCH.md HBM section)
@@ -36,7 +36,7 @@ def counter(db, name):
     return {k: (v[0] / v[1], v[1]) for k, v in acc.items()}
 
 
-def pmc(fetch_db, write_db, out, note=""):
+def pmc(fetch_db, write_db, out, note="", model=None, batch=None):
     fe, wr = counter(fetch_db, "FETCH_SIZE"), counter(write_db, "WRITE_SIZE")
     res = {}
     for k, (f, n) in fe.items():
@@ -44,11 +44,16 @@ def pmc(fetch_db, write_db, out, note=""):
         res[k] = {"launches": n, "FETCH_SIZE_KB_avg": f, "WRITE_SIZE_KB_avg": w,
                   "traffic_bytes": 2 * f * 1024 + w * 1024}
     with open(out, "w") as fo:
-        json.dump({"_how": note, "kernels": res}, fo, indent=1)
+        head = {"_how": note}
+        if model:
+            head["model"] = model
+        if batch:
+            head["batch"] = int(batch)
+        json.dump({**head, "kernels": res}, fo, indent=1)
 
 
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3])
     else:
-        pmc(sys.argv[2], sys.argv[3], sys.argv[4], sys.argv[5] if len(sys.argv) > 5 else "")
+        pmc(*sys.argv[2:5], *sys.argv[5:8])
