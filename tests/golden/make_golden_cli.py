@@ -28,6 +28,7 @@ CFG = (768, 2048, 12, 12, 12, 32000, 1024)  # stories110M shape
 SHARED = 0  # an unshared classifier: a random-init shared one makes every greedy continuation repeat its last token
 SEED = 110
 N_PROMPTS = 128
+NEAR_TIE = 1e-3  # greedy steps whose top-2 logit margin is below this are recorded (near_ties)
 PROMPTS_FILE = os.path.join(HERE, "gen_in_128.txt")
 TOK = os.path.join(HERE, "tokenizer.bin")
 OUT = os.path.join(HERE, "cli_gen_in_128_greedy.json")
@@ -47,12 +48,15 @@ def decode_one(args):
     m = O.Model(CFG, SHARED, seed=SEED)
     tok = H.Tokenizer(TOK, CFG[5])
     ids = tok.encode(prompt)
-    token, pos, text, gen = ids[0], 0, b"", []
+    token, pos, text, gen, near = ids[0], 0, b"", [], []
     while True:
         lg = m.forward(token, pos)
         nxt = ids[pos + 1] if pos < len(ids) - 1 else int(np.argmax(lg))  # sample_argmax: lowest index on ties
         if pos >= len(ids) - 1:
             gen.append(nxt)
+            top = np.sort(lg.astype(np.float64))[-2:]
+            if top[1] - top[0] < NEAR_TIE:  # a near-tie: [pos, margin, text offset before this token]
+                near.append([pos, float(top[1] - top[0]), len(text)])
         pos += 1
         if nxt in (1, 2):
             break
@@ -61,7 +65,7 @@ def decode_one(args):
         token = nxt
         if pos >= CFG[6]:
             break
-    return idx, text + b"\n", pos - 1, gen
+    return idx, text + b"\n", pos - 1, gen, near
 
 
 def main():
@@ -74,7 +78,11 @@ def main():
            "n_prompts": len(ps), "batch_independent": True,
            "output_file": body.decode("latin-1"), "total_achieved_tokens": sum(r[2] for r in res),
            "generated_tokens": [r[3] for r in res],
-           "outputs": [r[1].decode("latin-1") for r in res], "achieved_tokens": [r[2] for r in res]}
+           "outputs": [r[1].decode("latin-1") for r in res], "achieved_tokens": [r[2] for r in res],
+           "near_ties": [r[4] for r in res],
+           "near_ties_doc": "per prompt: [position, top-2 margin, byte offset of that token's piece in the output] "
+                            "of every greedy step with margin < NEAR_TIE; a GPU decode within the fp32 tolerance may "
+                            "take the other branch there (tests/test_cli_gpu.py)"}
     with open(OUT, "w") as f:
         json.dump(out, f)
     print(f"{len(ps)} prompts, {out['total_achieved_tokens']} tokens", file=sys.stderr)
