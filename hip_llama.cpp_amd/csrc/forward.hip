@@ -139,6 +139,8 @@ struct thallama_decoder {
   float* part_d = nullptr;      // attention partials [B][H][<=16 units][hs+4]
   unsigned* cnt_d = nullptr;    // attention combine tickets [B][H]
   bool q8 = false;              // int8 (runq Q8_0) weights in w8; w then holds only norms + embedding
+  bool q8x = false;             // int8 multi-launch steps in runq's arithmetic order (q8_exact.hip)
+  float* q8att_d = nullptr;     //   their attention scores [B][H][S]
   Q8TransformerWeights w8 = {};
   int nsplit = 1;
   bool nt = true;
@@ -387,6 +389,7 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   (void)hipFree(d->ssq_d);
   (void)hipFree(d->mpart_d);
   (void)hipFree(d->xq_d);
+  (void)hipFree(d->q8att_d);
   (void)hipFree(d->xqs_d);
   (void)hipFree(d->hq_d);
   (void)hipFree(d->hqs_d);
@@ -445,6 +448,7 @@ static hipError_t gemv(thallama_decoder* d, int mode, tl::GemvParams& p, const Q
     p.xq = d->xq_d;
     p.xqs = d->xqs_d;
   }
+  if (d->q8x) return tl::launch_gemv_q8_exact(mode, p, d->stream, d->nt);
   return tl::launch_gemv_q8(mode, p, d->stream, d->nt);
 }
 #define Q8L(name) (d->q8 ? &d->w8.name[l] : nullptr)
@@ -453,7 +457,7 @@ static hipError_t gemv(thallama_decoder* d, int mode, tl::GemvParams& p, const Q
 // output row quantised as well (attention.hpp: store_head), the codes Wo's quantise pass would
 // have produced from the same floats, so that pass is skipped
 static int q8_attn_quant(const thallama_decoder* d) {
-  return d->q8 && d->xq_d && d->B >= 2 && d->B <= 8 && d->w8.group_size == 64 &&
+  return d->q8 && !d->q8x && d->xq_d && d->B >= 2 && d->B <= 8 && d->w8.group_size == 64 &&
          (d->hs == 64 || d->hs == 128 || d->hs == 256) && (d->dim % 64) == 0;
 }
 
@@ -466,7 +470,7 @@ static int q8_ffn_quant(const thallama_decoder* d) {
     const char* e = getenv("THALLAMA_Q8_FFN_QUANT");
     return e && atoi(e) != 0;
   }();
-  return on && d->q8 && tl::q8_swiglu_quant_ok(d->B, d->w8.group_size, d->dim, d->hidden);
+  return on && d->q8 && !d->q8x && tl::q8_swiglu_quant_ok(d->B, d->w8.group_size, d->dim, d->hidden);
 }
 
 // Enqueue one decode step reading tok_d / pos_d; logits land in s.logits.
@@ -565,7 +569,10 @@ static int enqueue_step(thallama_decoder* d) {
       const int lpk = d->hs / 4;
       const size_t lds = 64 + (size_t)(S > 1024 ? S : 1024) * 4;
       int ev = prof_begin(d);
-      if (d->hs == 64 || d->hs == 128 || d->hs == 256) {
+      if (d->q8x) {
+        // int8 in runq's order: scores, softmax and the column chains of q8_exact.hip
+        TL_TRY(tl::launch_attn_q8_exact(a, d->B, d->q8att_d, d->stream));
+      } else if (d->hs == 64 || d->hs == 128 || d->hs == 256) {
         // wave-level units, in-kernel combine (attention.hpp: attn_wave_kernel)
         tl::AttnWaveParams wp = {};
         wp.a = a;
@@ -1208,6 +1215,19 @@ extern "C" int thallama_decoder_create_q8(thallama_decoder** out, const Config* 
   thallama_decoder* d = *out;
   d->q8 = true;
   d->w8 = *w8;
+  {  // runq's arithmetic order on the multi-launch steps (env THALLAMA_Q8_EXACT=0: the faster
+     // reordered kernels, logits within the Q8 tolerance instead)
+    const char* e = getenv("THALLAMA_Q8_EXACT");
+    d->q8x = !(e && e[0] == '0') && batch <= 8 && tl::q8_exact_ok(w8->group_size, d->dim, d->hidden, d->hs, d->S);
+  }
+  if (d->q8x) {
+    TL_TRY(hipMalloc(&d->q8att_d, sizeof(float) * (size_t)batch * d->H * d->S));
+    if (batch < 2) {  // (batch 1 multi-launch: the quantised activations' scratch too)
+      const size_t kmax = (size_t)(d->dim > d->hidden ? d->dim : d->hidden);
+      TL_TRY(hipMalloc(&d->xq_d, 8 * kmax));
+      TL_TRY(hipMalloc(&d->xqs_d, sizeof(float) * 8 * (kmax / 16 + 1)));
+    }
+  }
   if (batch >= 2) {
     const size_t kmax = (size_t)(d->dim > d->hidden ? d->dim : d->hidden);
     TL_TRY(hipMalloc(&d->xq_d, 8 * kmax));

@@ -201,6 +201,10 @@ class Model:
         lib().oracle_greedy(self.h, token, pos0, n, out)
         return list(out)
 
+    def logits(self):
+        """The logits of the last forward (a copy)."""
+        return np.ctypeslib.as_array(lib().oracle_model_logits(self.h), shape=(self.vocab,)).copy()
+
     def buf(self, which, n):
         """RunState buffer after a forward: 0 x, 1 xb, 2 xb2, 3 hb, 4 hb2, 5 q, 6 k, 7 v (diagnostics)."""
         return np.ctypeslib.as_array(lib().oracle_model_buf(self.h, which), shape=(n,)).copy()

@@ -101,21 +101,29 @@ def f32bits_of(d):
 
 
 @pytest.mark.parametrize("name", ["stories110m_shared", "stories110m_unshared", "llama2_7b"])
-def test_int8_256_step_greedy_bitexact_vs_runq(gpu, name):
-    """BASELINE configs[3]: the int8 (runq) greedy decode on the persistent step — every one of the
-    256 tokens equals runq's, and the last step's logits are bit-identical to runq's (the 110M
-    unshared case includes a step whose top-2 margin is 1.2e-6: only exact arithmetic holds it)."""
+@pytest.mark.parametrize("path", ["persistent", "multilaunch", "batch8", "batch3"])
+def test_int8_256_step_greedy_bitexact_vs_runq(gpu, name, path):
+    """BASELINE configs[3]: the int8 (runq) greedy decode — every one of the 256 tokens equals
+    runq's, and the last step's logits are bit-identical to runq's (the 110M unshared case includes
+    a step whose top-2 margin is 1.2e-6: only exact arithmetic holds it).  Paths: the batch-1
+    persistent step, and the multi-launch steps in runq's order (q8_exact.hip) at batch 1, 3 and 8
+    (config[4]'s per-GPU shape with int8 weights): every sequence of the batch."""
     case = CASES[name]
     g = case["q8"]
-    keep, dec = q8_decoder(gpu, case, 1)
+    B = 8 if path == "batch8" else 3 if path == "batch3" else 1
+    keep, dec = q8_decoder(gpu, case, B)
     dec.set(gpu.OPT_USE_GRAPH, 1)
-    assert dec.persistent()
-    got = dec.greedy([case["start_token"]], [case["start_pos"]], case["steps"])[:, 0].tolist()
-    first = next((i for i, (a, w) in enumerate(zip(got, g["tokens"])) if a != w), None)
-    assert first is None, (f"{name} int8: token {first} differs (got {got[first]}, runq {g['tokens'][first]}, "
-                           f"runq top-2 margin there {g['margins'][first]:.3g})")
-    lg = dec.logits()[0]
-    np.testing.assert_array_equal(lg.view(np.uint32), LAST[name + "_q8_last"].view(np.uint32))
+    if path == "multilaunch":
+        dec.set(gpu.OPT_PERSISTENT, 0)
+    assert dec.persistent() == (path == "persistent")
+    got = dec.greedy([case["start_token"]] * B, [case["start_pos"]] * B, case["steps"])
+    for b in range(B):
+        seq = got[:, b].tolist()
+        first = next((i for i, (a, w) in enumerate(zip(seq, g["tokens"])) if a != w), None)
+        assert first is None, (f"{name} int8 {path} seq {b}: token {first} differs (got {seq[first]}, runq "
+                               f"{g['tokens'][first]}, runq top-2 margin there {g['margins'][first]:.3g})")
+        lg = dec.logits()[b]
+        np.testing.assert_array_equal(lg.view(np.uint32), LAST[name + "_q8_last"].view(np.uint32))
 
 
 @pytest.mark.parametrize("name", ["stories110m_unshared", "llama2_7b"])

@@ -149,11 +149,14 @@ def test_q8_drift_is_bounded(gpu, oracle):
 
 @pytest.mark.parametrize("cfg,B", [(SMALL_GQA, 2), (SMALL_GQA, 3), (SMALL_GQA, 4), (SMALL_GQA, 8),
                                    ((768, 2048, 2, 12, 12, 4096, 256), 5), ((1024, 2048, 2, 8, 4, 4096, 256), 6)])
-def test_q8_batched_decoder_matches_runq(gpu, oracle, cfg, B):
-    """4..8 sequences take the int8 matrix-core GEMV (gemv_q8_mfma.hpp): exact int32 group dots
-    by v_mfma_i32_16x16x64_i8, scaled per group in fp32; 2..3 take the dot4 kernel.  Attention
-    stores its output quantised for Wo (head sizes 64 and 128 here).  Teacher-forced logits of every sequence
-    (own tokens, own positions) against runq's forward, within Q8_TOL."""
+def test_q8_batched_decoder_matches_runq(gpu, oracle, cfg, B, monkeypatch):
+    """The REORDERED batched int8 kernels (THALLAMA_Q8_EXACT=0; the default path is runq-exact,
+    tests/test_q8_exact_gpu.py): 4..8 sequences take the int8 matrix-core GEMV (gemv_q8_mfma.hpp):
+    exact int32 group dots by v_mfma_i32_16x16x64_i8, scaled per group in fp32, K split across
+    blocks; 2..3 take the dot4 kernel.  Attention stores its output quantised for Wo (head sizes 64
+    and 128 here).  Teacher-forced logits of every sequence (own tokens, own positions) against
+    runq's forward, within Q8_TOL."""
+    monkeypatch.setenv("THALLAMA_Q8_EXACT", "0")
     c = gpu.Config.make(*cfg)
     q = gpu.DeviceModelQ8(c, 0, 64, from_model=gpu.DeviceModel(c, 0, seed=11))
     dec = gpu.Decoder(q, gpu.DeviceState(c, B))
