@@ -349,8 +349,10 @@ def main(argv=None):
             # the first of these the PMC pass saw
             pre = "gemv_q8" if q8 else "gemv"
             cands = [f"{pre}_rr_kernel", f"{pre}_mfma_kernel", f"{pre}_kernel"] if B >= 4 else [f"{pre}_kernel"]
+            if q8:  # the batched int8 step runs in runq's order by default (q8_exact.hip)
+                cands = [f"{pre}_exact_kernel"] + cands
             seen = [c for c in cands if any(k.startswith(f"void tl::{c}<2") for k in pmc.get("kernels", {}))]
-            kname = seen[0] if seen else (f"{pre}_mfma_kernel" if B > 4 else cands[0])
+            kname = seen[0] if seen else (cands[0] if q8 else f"{pre}_mfma_kernel" if B > 4 else cands[0])
             roof = {"bound": "hbm", "achieved": round(ffn["GBps"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ffn["GBps"] / HBM_PEAK_GBS, 4),
                     "traffic": traffic_of(f"void tl::{kname}<2") if pmc else None,

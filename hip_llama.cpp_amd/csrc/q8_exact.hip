@@ -207,14 +207,19 @@ __global__ void __launch_bounds__(W * 64) gemv_q8_exact_kernel(GemvParams p) {
     asm volatile("" ::: "memory");
   };
 
-  Run ta, tb;
+  // three runs in flight per wave (one block per CU: the LDS holds every product of the tile)
+  Run ta, tb, tc;
   if (nrun > 0) load(ta, 0);
-  for (int g = 0; g < nrun; g += 2) {
-    if (g + 1 < nrun) load(tb, g + 1);
+  if (nrun > 1) load(tb, 1);
+  for (int g = 0; g < nrun; g += 3) {
+    if (g + 2 < nrun) load(tc, g + 2);
     mma(ta, g);
     if (g + 1 >= nrun) break;
-    if (g + 2 < nrun) load(ta, g + 2);
+    if (g + 3 < nrun) load(ta, g + 3);
     mma(tb, g + 1);
+    if (g + 2 >= nrun) break;
+    if (g + 4 < nrun) load(tb, g + 4);
+    mma(tc, g + 2);
   }
   __syncthreads();  // every product is in LDS; the staging tiles become the row-value buffer
   // runq.c:330-338: each (row, sequence) value is the left-to-right chain over its groups
