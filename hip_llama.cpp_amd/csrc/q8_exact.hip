@@ -36,51 +36,69 @@ namespace tl {
 // seqsum layout of K squares (when p.rms_w).
 __global__ void __launch_bounds__(256) q8x_prequant_kernel(GemvParams p) {
   keep_implicit_args();
+  constexpr int MR = 3;  // 16-value slices per thread (K <= 3 * 256 * 16 = 12288)
   extern __shared__ __attribute__((aligned(16))) float q8x_sq[];
   __shared__ float s_sum;
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63;
   const int K = p.K, n16 = K >> 4, ng = K >> 6;
   const float* src = p.tok ? p.emb + (long long)p.tok[b] * K : p.x + b * p.x_stride;
+  // every value loaded once, up front, and kept in registers through the norm
+  f4 v[MR][4];
+#pragma unroll
+  for (int r = 0; r < MR; ++r) {
+    const int sl = r * 256 + t;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[r][u] = sl < n16 ? reinterpret_cast<const f4*>(src + sl * 16)[u] : f4{0.f, 0.f, 0.f, 0.f};
+  }
   if (p.tok)
-    for (int j = t; j < (K >> 2); j += 256)
-      reinterpret_cast<f4*>(p.x_out + b * p.x_stride)[j] = reinterpret_cast<const f4*>(src)[j];
+#pragma unroll
+    for (int r = 0; r < MR; ++r)
+      if (r * 256 + t < n16)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) reinterpret_cast<f4*>(p.x_out + b * p.x_stride + (r * 256 + t) * 16)[u] = v[r][u];
   float s = 1.f;
   if (p.rms_w) {
     const int ch = seqsum_ch(K);
     for (int i = t; i < seqsum_floats(K); i += 256) q8x_sq[i] = 0.f;  // the padding adds +0
     __syncthreads();
-    for (int j = t; j < (K >> 2); j += 256) {  // runq.c:286: x[j] * x[j], one rounding each
-      const f4 v = reinterpret_cast<const f4*>(src)[j];
-      float* d = q8x_sq + seqsum_index(4 * j, ch);  // ch % 4 == 0: the four land in one chunk
-      d[0] = __fmul_rn(v.x, v.x); d[1] = __fmul_rn(v.y, v.y); d[2] = __fmul_rn(v.z, v.z); d[3] = __fmul_rn(v.w, v.w);
+#pragma unroll
+    for (int r = 0; r < MR; ++r) {
+      const int sl = r * 256 + t;
+      if (sl < n16)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {  // runq.c:286: x[j] * x[j], one rounding each
+          float* d = q8x_sq + seqsum_index(sl * 16 + 4 * u, ch);  // ch % 4 == 0: one chunk
+          d[0] = __fmul_rn(v[r][u].x, v[r][u].x); d[1] = __fmul_rn(v[r][u].y, v[r][u].y);
+          d[2] = __fmul_rn(v[r][u].z, v[r][u].z); d[3] = __fmul_rn(v[r][u].w, v[r][u].w);
+        }
     }
     __syncthreads();
     if (t < 64) {
-      const float v = K <= 4096 ? wave_seqsum_reg(q8x_sq, K, lane) : wave_seqsum(q8x_sq, K, lane);
-      if (lane == 0) s_sum = v;
+      const float sum = K <= 4096 ? wave_seqsum_reg(q8x_sq, K, lane) : wave_seqsum(q8x_sq, K, lane);
+      if (lane == 0) s_sum = sum;
     }
     __syncthreads();
     s = __fdiv_rn(1.0f, sqrtf(__fadd_rn(__fdiv_rn(s_sum, (float)K), 1e-5f)));  // runq.c:287-289
   }
   // 4 threads per group of 64, 16 values each (gemv_q8_prequant_reg_kernel's arithmetic)
-  for (int sl0 = 0; sl0 < n16; sl0 += 256) {
-    const int sl = sl0 + t;
-    const bool live = sl < n16;
-    f4 v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      v[u] = live ? reinterpret_cast<const f4*>(src + sl * 16)[u] : f4{0.f, 0.f, 0.f, 0.f};
-      if (live && p.rms_w) v[u] = rms_apply(v[u], reinterpret_cast<const f4*>(p.rms_w + sl * 16)[u], s);
-    }
+  for (int r = 0; r < MR; ++r) {
+    if (r * 256 >= n16) break;  // block-uniform
+    const int sl = r * 256 + t;
+    const bool live = sl < n16;
+    f4 w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      w[u] = live && p.rms_w ? rms_apply(v[r][u], reinterpret_cast<const f4*>(p.rms_w + sl * 16)[u], s) : v[r][u];
     float m = 0.f;
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(w[u].x), fabsf(w[u].y)), fmaxf(fabsf(w[u].z), fabsf(w[u].w))));
     m = fmaxf(m, dpp_f<0xB1>(m));
     m = fmaxf(m, dpp_f<0x4E>(m));
     const float scale = __fdiv_rn(m, 127.0f);
     if (live) {
-      *reinterpret_cast<q8i4*>(p.xq + (long long)b * K + sl * 16) = q8_pack16(v, scale);
+      *reinterpret_cast<q8i4*>(p.xq + (long long)b * K + sl * 16) = q8_pack16(w, scale);
       if ((sl & 3) == 0) p.xqs[(long long)b * ng + (sl >> 2)] = scale;
     }
   }
@@ -287,7 +305,7 @@ static hipError_t launch_q8x_mode(const GemvParams& p0, hipStream_t s, bool nt) 
 }
 
 bool q8_exact_ok(int gs, int dim, int hidden, int hs, int seq_len) {
-  return gs == 64 && dim % 256 == 0 && hidden % 256 == 0 && (hs == 64 || hs == 128) &&
+  return gs == 64 && dim % 256 == 0 && hidden % 256 == 0 && (hs == 64 || hs == 128) && hidden <= 12288 &&
          q8x_gemv_lds(1, hidden, 4) <= 160 * 1024 - 256 && seq_len <= 8192;
 }
 
