@@ -59,6 +59,9 @@ constexpr int NSW = PW - 1;  // streaming waves per block
 constexpr int SB = 4;        // staged float4 per thread and batch (granule loads in flight)
 constexpr int kPResidFloats = 256;  // residual-stream slice per block (LDS)
 constexpr unsigned kSpinLimit = 1u << 18;
+#ifndef PERSIST_ATTN_CH
+#define PERSIST_ATTN_CH 16  // keys per attention chunk (one memory latency each) in the control wave
+#endif
 #ifndef PERSIST_XCD_SKEW
 #define PERSIST_XCD_SKEW 4
 #endif
@@ -739,7 +742,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
             attn_unit_split<HS>(aw, u / p.ang, u % p.ang, p.ang, scr, reinterpret_cast<float*>(xs), p.pad_floats, lane);
         } else {
           const int units = p.H * p.NS;
-          for (int u = blockIdx.x; u < units; u += G) attn_unit<HS, 16, true>(aw, u, lane);
+          for (int u = blockIdx.x; u < units; u += G) attn_unit<HS, PERSIST_ATTN_CH, true>(aw, u, lane);
         }
         TRACE(3);
         continue;
@@ -971,11 +974,17 @@ bool persistent_prepare(PStep& p, int ncu, const char** why) {
   return true;
 }
 
-// Co-residency of the grid (one block per CU, spin-waiting on each other's hand-offs) is
-// GUARANTEED by a cooperative launch: the runtime dispatches it on a cooperative queue, which
-// starts the grid only when every block can be resident at once, and refuses (hipErrorCooperative
-// LaunchTooLarge) a grid that could never be.  The bounded waits stay as a second line of
-// defence.  THALLAMA_PERSIST_COOP=0 selects a plain launch (measurement only).
+// Co-residency of the grid (one block per CU, spin-waiting on each other's hand-offs): a direct
+// launch is cooperative — the runtime dispatches it on a cooperative queue, which starts the grid
+// only when every block can be resident at once, and refuses (hipErrorCooperativeLaunchTooLarge)
+// a grid that could never be.  The greedy loop captures the step into a hipGraph; a captured
+// cooperative launch replays cooperatively on ROCm 7.2 (MI355X_MICROARCH.md, residency: +17-20 us
+// per replay, although hipKernelNodeAttributeCooperative reads 0) — an observation, not an API
+// guarantee, so what holds in every case is the rest: the grid is sized by the occupancy query
+// (one block per CU), every wait is bounded, and a launch whose waits gave up is reported and
+// re-run on the multi-launch step (tests/test_persist_gpu.py, test_persist_b_gpu.py
+// test_give_up_falls_back: a launch missing a block, eager and from a graph).
+// THALLAMA_PERSIST_COOP=0 selects a plain launch (measurement only).
 static bool use_cooperative() {
   static const bool on = [] {
     const char* e = getenv("THALLAMA_PERSIST_COOP");

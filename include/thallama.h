@@ -46,8 +46,10 @@ enum {
 /* 1 if the decoder runs its steps as one persistent launch (THALLAMA_OPT_PERSISTENT
  * requested and the shape supported), else 0. */
 int thallama_decoder_persistent(thallama_decoder* d);
-/* 1 if the persistent step is dispatched as a cooperative launch (grid co-residency guaranteed
- * by the runtime), 0 for a plain launch (THALLAMA_PERSIST_COOP=0 or no device support). */
+/* 1 if the persistent step is dispatched as a cooperative launch (the runtime checks the grid's
+ * co-residency; replays of a captured step keep cooperative dispatch on ROCm 7.2 by observation,
+ * and every wait is bounded either way), 0 for a plain launch (THALLAMA_PERSIST_COOP=0 or no
+ * device support). */
 int thallama_persistent_cooperative(void);
 /* Diagnostics: the persistent step's hand-off granules ({value, tag}: x | xb | hb | q k v | int8
  * codes | scales; the last layer's after a launch) into host[n]; returns the count (host NULL:
