@@ -637,6 +637,180 @@ TL_DEVICE void attn_unit_split(const AttnWaveParams& w, int h, int c, int NG, fl
   wave_lds_fence();  // the strip and window are rewritten by the next unit
 }
 
+// fp32 persistent step (batch 1): attn_unit with the keys in LDS windows.  attn_unit holds one
+// 16-key chunk in registers per memory latency, so at long contexts a unit's key range (T / NS
+// keys) is a chain of latencies (7B at position 2000: ~15 chunks, ~30 us per layer).  Here the
+// unit's keys come in rounds of up to 64: K rows transposed (piece i of key l at kw[i * 256 + 4 l])
+// and V rows (vw[u * HS + c]) by LDS-DMA, all of a round requested at once — one latency per 64
+// keys; one lane per key for the scores, online softmax across rounds, a lane's VPL columns for
+// the output.  Unit s of (b, h) takes the contiguous keys [T s / nact, T (s+1) / nact); the last
+// row (T-1, written by this launch's QKV phase) comes from the granules.  Partials combine as in
+// attn_unit (same records and tickets).  win: attn_win_floats(HS) floats of LDS.
+__host__ __device__ constexpr int attn_win_floats(int hs) { return 2 * 64 * hs + 2 * hs; }
+
+template <int HS>
+TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int lane) {
+  constexpr int VPL = HS / 64;
+  constexpr int PC = HS / 4;     // 16-B pieces per row
+  constexpr int RPI = 256 / HS;  // V rows per 1-KiB DMA instruction
+  const AttnParams& p = w.a;
+  const int BH = w.B * p.n_heads;
+  const int s = unit / BH, bh = unit % BH;
+  const int b = bh / p.n_heads, h = bh % p.n_heads;
+  const int T = p.pos[b] + 1;
+  const int nact = min(w.NS, (T + 15) / 16);  // live units for this (b, h): >= 16 keys each
+  if (s >= nact) return;
+  const int k0 = (int)((long long)T * s / nact), k1 = (int)((long long)T * (s + 1) / nact);
+  const int tc = T - 1;  // cached rows [0, T-1); row T-1 from the granules
+  const int kvh = h / p.kv_mul;
+  const float* kbase = p.kc + (long long)b * p.kv_b_stride + p.kv_l_off + (long long)kvh * HS;
+  const float* vbase = p.vc + (long long)b * p.kv_b_stride + p.kv_l_off + (long long)kvh * HS;
+  float* kw = win;              // [PC][256]: 64 keys transposed
+  float* vw = kw + 64 * HS;     // [64][HS]
+  float* qs = vw + 64 * HS;     // q [HS]
+  float* kn = qs + HS;          // k row T-1 [HS]
+  const int ke = min(k1, tc);   // cached keys of this unit: [k0, ke)
+  auto issue = [&](int t0, int n) {
+    if (lane < n) {
+      const float* row = kbase + (long long)(t0 + lane) * p.kv_dim;
+#pragma unroll
+      for (int i = 0; i < PC; ++i) dma16(row + 4 * i, kw + i * 256);
+    }
+    for (int j = 0; j * RPI < n; ++j) {
+      const int r = j * RPI + lane / PC;
+      if (r < n) dma16(vbase + (long long)(t0 + r) * p.kv_dim + (lane % PC) * 4, vw + j * 256);
+    }
+  };
+  if (k0 < ke) issue(k0, min(64, ke - k0));  // the first round is in flight before q has arrived
+  // q, and the new k / v row if this unit holds it, from the QKV phase's granules
+  const unsigned long long* gq = w.gqkv + (long long)b * (p.dim + 2 * p.kv_dim);
+  const unsigned long long* srcq = gq + h * HS;
+  const unsigned long long* srck = gq + p.dim + kvh * HS;
+  const unsigned long long* srcv = gq + p.dim + p.kv_dim + kvh * HS;
+  const bool last = k1 == T;
+  float vn[VPL];
+  {
+    unsigned long long g[3][VPL];
+#pragma unroll
+    for (int c = 0; c < VPL; ++c) {
+      g[0][c] = ld8_sc1(srcq + lane * VPL + c);
+      if (last) {
+        g[1][c] = ld8_sc1(srck + lane * VPL + c);
+        g[2][c] = ld8_sc1(srcv + lane * VPL + c);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < VPL; ++c) {
+      qs[lane * VPL + c] = (unsigned)(g[0][c] >> 32) == w.tag_in ? __uint_as_float((unsigned)g[0][c])
+                                                                  : gran_wait(srcq + lane * VPL + c, w.tag_in, w.err);
+      if (last) {
+        kn[lane * VPL + c] = (unsigned)(g[1][c] >> 32) == w.tag_in ? __uint_as_float((unsigned)g[1][c])
+                                                                    : gran_wait(srck + lane * VPL + c, w.tag_in, w.err);
+        vn[c] = (unsigned)(g[2][c] >> 32) == w.tag_in ? __uint_as_float((unsigned)g[2][c])
+                                                       : gran_wait(srcv + lane * VPL + c, w.tag_in, w.err);
+      }
+    }
+  }
+  wave_lds_fence();
+  const float rs = sqrtf((float)HS);
+  const f4* q4 = reinterpret_cast<const f4*>(qs);
+  float m = -3.402823466e+38f, l = 0.f;
+  float o[VPL];
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) o[c] = 0.f;
+  // one lane's dot of q with the HS floats at base + i * stride4 * 4 (piece i); 4 partial sums
+  auto dot = [&](const float* base, int stride4) {
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+    for (int i = 0; i < PC; ++i) a[i & 3] = dot4(q4[i], reinterpret_cast<const f4*>(base)[i * stride4], a[i & 3]);
+    return (a[0] + a[1]) + (a[2] + a[3]);
+  };
+  // fold n scores (lane t: key t; lanes >= n: none) and their V rows (vrow(t)) into (m, l, o)
+  auto fold = [&](float sc, int n, const float* vrows, int vstride) {
+    const float my = lane < n ? __fdiv_rn(sc, rs) : -3.402823466e+38f;
+    const float mn = fmaxf(m, wave_max_u(my));
+    const float e = lane < n ? expf_libm(__fsub_rn(my, mn)) : 0.f;
+    const float scale = expf_libm(__fsub_rn(m, mn));
+    l = fmaf(l, scale, wave_sum_u(e));
+#pragma unroll
+    for (int c = 0; c < VPL; ++c) o[c] *= scale;
+    for (int u = 0; u < n; ++u) {
+      const float a = lane_f(e, u);
+#pragma unroll
+      for (int c = 0; c < VPL; ++c) o[c] = fmaf(a, vrows[u * vstride + lane * VPL + c], o[c]);
+    }
+    m = mn;
+  };
+  for (int t0 = k0; t0 < ke; t0 += 64) {
+    const int n = min(64, ke - t0);
+    if (t0 > k0) {
+      wave_lds_fence();  // the previous round's reads are done before this round lands
+      issue(t0, n);
+    }
+    dma_wait_all();
+    fold(dot(kw + 4 * lane, 64), n, vw, HS);
+  }
+  if (last) {  // key T-1: every lane computes its score (one key), lane 0's counts
+    const float sc = dot(kn, 1);
+    // fold one key whose V row is vn (in registers): the same arithmetic inline
+    const float my = lane < 1 ? __fdiv_rn(sc, rs) : -3.402823466e+38f;
+    const float mn = fmaxf(m, wave_max_u(my));
+    const float e0 = expf_libm(__fsub_rn(lane_f(my, 0), mn));
+    const float scale = expf_libm(__fsub_rn(m, mn));
+    l = fmaf(l, scale, e0);
+#pragma unroll
+    for (int c = 0; c < VPL; ++c) o[c] = fmaf(e0, vn[c], o[c] * scale);
+    m = mn;
+  }
+  wave_lds_fence();  // the window is rewritten by the block's next unit
+  if (nact == 1) {
+#pragma unroll
+    for (int c = 0; c < VPL; ++c) o[c] = __fdiv_rn(o[c], l);
+    publish_head<HS>(w, b, h, o, lane);
+    return;
+  }
+  // publish this unit's partial (write-through), drain, take a ticket; the last unit combines
+  float* rec = p.part + ((long long)bh * w.NS + s) * (HS + 4);
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) st_sc1(rec + lane * VPL + c, o[c]);
+  if (lane == 0) {
+    st_sc1(rec + HS, m);
+    st_sc1(rec + HS + 1, l);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  unsigned ticket = 0;
+  if (lane == 0) ticket = __hip_atomic_fetch_add(w.cnt + bh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ticket = (unsigned)__builtin_amdgcn_readfirstlane((int)ticket);
+  if (ticket != (unsigned)(nact - 1)) return;
+  const float* recs = p.part + (long long)bh * w.NS * (HS + 4);
+  const int kl = lane < nact ? lane : nact - 1;
+  const float mk = ld_sc1(recs + kl * (HS + 4) + HS);
+  const float lk = ld_sc1(recs + kl * (HS + 4) + HS + 1);
+  float ov[kMaxNS][VPL];
+#pragma unroll
+  for (int k = 0; k < kMaxNS; ++k) {
+    const int kk = k < nact ? k : nact - 1;
+#pragma unroll
+    for (int c = 0; c < VPL; ++c) ov[k][c] = ld_sc1(recs + kk * (HS + 4) + lane * VPL + c);
+  }
+  const float M = wave_max_u(lane < nact ? mk : -3.402823466e+38f);
+  const float sk = lane < nact ? expf_libm(__fsub_rn(mk, M)) : 0.f;
+  const float L = wave_sum_u(lk * sk);
+  float acc[VPL];
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) acc[c] = 0.f;
+#pragma unroll
+  for (int k = 0; k < kMaxNS; ++k) {
+    const float a = lane_f(sk, k);
+#pragma unroll
+    for (int c = 0; c < VPL; ++c) acc[c] = fmaf(ov[k][c], a, acc[c]);
+  }
+#pragma unroll
+  for (int c = 0; c < VPL; ++c) acc[c] = __fdiv_rn(acc[c], L);
+  publish_head<HS>(w, b, h, acc, lane);
+  if (lane == 0) __hip_atomic_store(w.cnt + bh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // out[b][h*hs + i] = sum_s o_s[i] e^{m_s-M} / sum_s l_s e^{m_s-M}
 template <int kUnused = 0>
 __global__ void __launch_bounds__(256) attn_combine_kernel(AttnParams p) {

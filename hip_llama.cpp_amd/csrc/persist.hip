@@ -62,6 +62,9 @@ constexpr unsigned kSpinLimit = 1u << 18;
 #ifndef PERSIST_ATTN_CH
 #define PERSIST_ATTN_CH 16  // keys per attention chunk (one memory latency each) in the control wave
 #endif
+#ifndef PERSIST_ATTN_WIN
+#define PERSIST_ATTN_WIN 1  // fp32: attention units with their keys in LDS windows (attn_unit_win)
+#endif
 #ifndef PERSIST_XCD_SKEW
 #define PERSIST_XCD_SKEW 4
 #endif
@@ -704,7 +707,7 @@ TL_DEVICE void grid_barrier(const PStep& p) {
 template <int HS, bool ROLE0, bool Q8>
 TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xres, float* red,
                       float* rmsw, f4* xs, signed char* xq, float* xsc, float* sqa, float* scr, float* cwb,
-                      const uint64_t* etab, unsigned tb) {
+                      const uint64_t* etab, unsigned tb, float* awin) {
   const int G = gridDim.x;
   const int nph = 5 * p.L + 1;
   unsigned* ctr = reinterpret_cast<unsigned*>(red + 15);  // dynamic slot counter (red[0..PW) is the norm sum)
@@ -742,7 +745,10 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
             attn_unit_split<HS>(aw, u / p.ang, u % p.ang, p.ang, scr, reinterpret_cast<float*>(xs), p.pad_floats, lane);
         } else {
           const int units = p.H * p.NS;
-          for (int u = blockIdx.x; u < units; u += G) attn_unit<HS, PERSIST_ATTN_CH, true>(aw, u, lane);
+          for (int u = blockIdx.x; u < units; u += G) {
+            if constexpr (PERSIST_ATTN_WIN) attn_unit_win<HS>(aw, u, awin, lane);
+            else attn_unit<HS, PERSIST_ATTN_CH, true>(aw, u, lane);
+          }
         }
         TRACE(3);
         continue;
@@ -859,6 +865,7 @@ __global__ void __launch_bounds__(PT) persistent_step_kernel(PStep p) {
   float* scr = sqa + p.n_sqa;
   float* cwb = scr + p.n_scr;
   uint64_t* etab = reinterpret_cast<uint64_t*>(cwb + p.n_cw);  // the expf table (32 doubles' bits)
+  float* awin = reinterpret_cast<float*>(etab + 32);             // fp32: the attention window
   {
     constexpr uint64_t tab[32] = TL_EXPF_TABLE;
     if (threadIdx.x < 32) etab[threadIdx.x] = tab[threadIdx.x];  // (read after the first barrier)
@@ -866,13 +873,14 @@ __global__ void __launch_bounds__(PT) persistent_step_kernel(PStep p) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const unsigned tb = p.seq[0] << 12;  // tag base of this launch
-  if (wave == 0) phases<HS, true, Q8>(p, wave, lane, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, etab, tb);
-  else phases<HS, false, Q8>(p, wave, lane, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, etab, tb);
+  if (wave == 0) phases<HS, true, Q8>(p, wave, lane, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, etab, tb, awin);
+  else phases<HS, false, Q8>(p, wave, lane, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, etab, tb, awin);
 }
 
 static size_t lds_bytes(const PStep& p) {
   return (size_t)(kPResidFloats + kPResFloats + 16 + p.dim + p.pad_floats) * 4 + (size_t)p.q8_pad +
-         (size_t)p.q8_pad / 16 + (size_t)(p.n_sqa + p.n_scr + p.n_cw) * 4 + 32 * 8;
+         (size_t)p.q8_pad / 16 + (size_t)(p.n_sqa + p.n_scr + p.n_cw) * 4 + 32 * 8 +
+         (p.q8 || !PERSIST_ATTN_WIN ? 0 : (size_t)attn_win_floats(p.hs) * 4);
 }
 
 template <int HS, bool Q8>
