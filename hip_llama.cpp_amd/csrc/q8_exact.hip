@@ -23,12 +23,31 @@
 //    RoPE from the host-libm table; residual adds are single roundings.
 #include <hip/hip_runtime.h>
 #include <mutex>
+#include <utility>
+#include <vector>
 #include "attention.hpp"
 #include "gemv_q8.hpp"
 #include "gemv_q8_mfma.hpp"
 #include "q8_dispatch.hpp"
 
 namespace tl {
+
+// Raise a kernel's dynamic-LDS limit to 160 KiB on the current device, once per (kernel, device):
+// the attribute is per device, and the CLI creates decoders on several devices from several
+// threads (app/run.cpp).
+static hipError_t lds_attr(const void* fn) {
+  static std::mutex mu;
+  static std::vector<std::pair<const void*, int>> done;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lock(mu);
+  for (const auto& d : done)
+    if (d.first == fn && d.second == dev) return hipSuccess;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e == hipSuccess) done.emplace_back(fn, dev);
+  return e;
+}
 
 // ---------------------------------------------------------------- activation quantisation
 // One block per sequence: x (or the token's embedding row, also copied to x_out) -> RMSNorm
@@ -266,12 +285,7 @@ __global__ void __launch_bounds__(W * 64) gemv_q8_exact_kernel(GemvParams p) {
 
 template <int MODE, bool NT, int W>
 static hipError_t launch_q8x_w(const GemvParams& p, hipStream_t s, size_t lds) {
-  static std::once_flag once;
-  static hipError_t attr = hipSuccess;
-  std::call_once(once, [] {
-    attr = hipFuncSetAttribute((const void*)gemv_q8_exact_kernel<MODE, NT, W>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  });
+  const hipError_t attr = lds_attr((const void*)gemv_q8_exact_kernel<MODE, NT, W>);
   if (attr != hipSuccess) return attr;
   const int rows = MODE == GM_QKV ? 2 * p.n_items : p.n_items;
   hipLaunchKernelGGL((gemv_q8_exact_kernel<MODE, NT, W>), dim3((rows + 15) / 16), dim3(W * 64), lds, s, p);
@@ -448,12 +462,7 @@ static hipError_t launch_attn_q8x_hs(const AttnParams& a, int B, float* att, hip
   if (e != hipSuccess) return e;
   const int rv = 256;  // V rows per round (a multiple of 16 and of the rows per DMA instruction)
   const size_t lds = (size_t)(64 + ((a.seq_len + 3) & ~3) + 64 * (4 * ((a.seq_len + 255) >> 8) + 4) + rv * CW) * 4;
-  static std::once_flag once;
-  static hipError_t attr = hipSuccess;
-  std::call_once(once, [] {
-    attr = hipFuncSetAttribute((const void*)attn_q8x_out_kernel<HS, NG>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               160 * 1024);
-  });
+  const hipError_t attr = lds_attr((const void*)attn_q8x_out_kernel<HS, NG>);
   if (attr != hipSuccess) return attr;
   hipLaunchKernelGGL((attn_q8x_out_kernel<HS, NG>), dim3(B * a.n_heads, NG), dim3(64), lds, s, a, att, rv);
   return hipGetLastError();
