@@ -136,6 +136,10 @@ struct thallama_decoder {
   unsigned* hcnt_d = nullptr;   //   and one ticket per 64-row group (zero between launches)
   float* mpart_d = nullptr;     // matrix-core GEMV split-K partial tiles
   unsigned* mcnt_d = nullptr;   //   and their tickets
+  float* mbpart_d = nullptr;    // 4x4x1 matrix-core GEMV (gemv_mb.hpp): partial-tile slabs
+  unsigned* mbcnt_d = nullptr;  //   and one ticket per 4-row group
+  long long mbpart_n = 0;
+  int mbcnt_n = 0;
   float* part_d = nullptr;      // attention partials [B][H][<=16 units][hs+4]
   unsigned* cnt_d = nullptr;    // attention combine tickets [B][H]
   bool q8 = false;              // int8 (runq Q8_0) weights in w8; w then holds only norms + embedding
@@ -331,6 +335,13 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
     TL_TRY(hipMalloc(&d->mpart_d, sizeof(float) * nblk * 2 * 256));
     TL_TRY(hipMalloc(&d->mcnt_d, sizeof(unsigned) * nblk));
     TL_TRY(hipMemset(d->mcnt_d, 0, sizeof(unsigned) * nblk));
+    int rows = d->V > d->hidden ? d->V : d->hidden;
+    rows = rows > d->dim + 2 * d->kv_dim ? rows : d->dim + 2 * d->kv_dim;
+    d->mbcnt_n = rows / 4 + 64;
+    d->mbpart_n = 4LL << 20;
+    TL_TRY(hipMalloc(&d->mbpart_d, sizeof(float) * (size_t)d->mbpart_n));
+    TL_TRY(hipMalloc(&d->mbcnt_d, sizeof(unsigned) * (size_t)d->mbcnt_n));
+    TL_TRY(hipMemset(d->mbcnt_d, 0, sizeof(unsigned) * (size_t)d->mbcnt_n));
   }
   {
     const size_t nsmax = (size_t)((d->S + kAttnChunk - 1) / kAttnChunk);
@@ -395,6 +406,8 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   (void)hipFree(d->hqs_d);
   (void)hipFree(d->hcnt_d);
   (void)hipFree(d->mcnt_d);
+  (void)hipFree(d->mbpart_d);
+  (void)hipFree(d->mbcnt_d);
   (void)hipFree(d->part_d);
   (void)hipFree(d->cnt_d);
   (void)hipFree(d->psync);
@@ -435,6 +448,10 @@ static hipError_t gemv(thallama_decoder* d, int mode, tl::GemvParams& p, const Q
   if (!d->q8) {
     p.mpart = d->mpart_d;
     p.mcnt = d->mcnt_d;
+    p.mbpart = d->mbpart_d;
+    p.mbcnt = d->mbcnt_d;
+    p.mbpart_floats = d->mbpart_n;
+    p.mbcnt_n = d->mbcnt_n;
     return tl::launch_gemv(mode, p, d->stream, d->nt);
   }
   p.Q0 = t0 ? t0->q : nullptr;
@@ -484,6 +501,7 @@ static int q8_ffn_quant(const thallama_decoder* d) {
 // matrix path ignore ssq_in (the streaming kernels normalise from x).
 static bool ssq_carry_ok(const thallama_decoder* d) {
   if (d->q8 || !d->ssq_d || d->no_ssq || (d->dim + 15) / 16 > 256) return false;  // (the kernel sums <= 256 tiles)
+  if (d->mbpart_d && tl::gemv_mb_takes(d->B)) return false;  // gemv_mb.hpp normalises in-block, keeps no sums
   for (int l = 0; l < d->L; ++l) {
     tl::GemvParams wo = {}, w2 = {};
     wo.W0 = d->w.wo + (long long)l * d->dim * d->dim;

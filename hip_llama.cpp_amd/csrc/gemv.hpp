@@ -91,6 +91,12 @@ struct GemvParams {
   float* ssq_out;
   const float* ssq_in;
   int ssq_nt;            // tiles of the producing launch (its rows / 16)
+  // optional scratch of the 4x4x1 matrix-core path (gemv_mb.hpp): partial-tile slabs of row groups
+  // cut between waves, and one ticket per 4-row group (zero between launches)
+  float* mbpart;
+  unsigned* mbcnt;
+  long long mbpart_floats;
+  int mbcnt_n;
 };
 
 // Blocks the matrix-core GEMV aims for: kMfmaDepth per CU (env THALLAMA_MFMA_DEPTH).
