@@ -670,18 +670,31 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
   float* qs = vw + 64 * HS;     // q [HS]
   float* kn = qs + HS;          // k row T-1 [HS]
   const int ke = min(k1, tc);   // cached keys of this unit: [k0, ke)
-  auto issue = [&](int t0, int n) {
-    if (lane < n) {
-      const float* row = kbase + (long long)(t0 + lane) * p.kv_dim;
+  // A round's K and V rows as exactly PC + 64 / RPI (= 2 PC) wave-instructions whatever its key
+  // count n (lanes past n re-read row t0 into slots nothing reads), so the waits below can count
+  // them: the next round's K rows land while this round's V rows are folded, its V rows while its
+  // scores are taken (K and V share no LDS, one window of each).
+  auto issue_k = [&](int t0, int n) {
+    const float* row = kbase + (long long)(t0 + (lane < n ? lane : 0)) * p.kv_dim;
 #pragma unroll
-      for (int i = 0; i < PC; ++i) dma16(row + 4 * i, kw + i * 256);
-    }
-    for (int j = 0; j * RPI < n; ++j) {
+    for (int i = 0; i < PC; ++i) dma16(row + 4 * i, kw + i * 256);
+  };
+  auto issue_v = [&](int t0, int n) {
+#pragma unroll
+    for (int j = 0; j < 64 / RPI; ++j) {
       const int r = j * RPI + lane / PC;
-      if (r < n) dma16(vbase + (long long)(t0 + r) * p.kv_dim + (lane % PC) * 4, vw + j * 256);
+      dma16(vbase + (long long)(t0 + (r < n ? r : 0)) * p.kv_dim + (lane % PC) * 4, vw + j * 256);
     }
   };
-  if (k0 < ke) issue(k0, min(64, ke - k0));  // the first round is in flight before q has arrived
+  static_assert(64 / RPI == PC, "K and V rounds are the same instruction count");
+  auto wait_all_but_round_half = [] {  // every DMA but the last PC instructions landed
+    if constexpr (PC == 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  };
+  if (k0 < ke) {  // the first round is in flight before q has arrived
+    issue_k(k0, min(64, ke - k0));
+    issue_v(k0, min(64, ke - k0));
+  }
   // q, and the new k / v row if this unit holds it, from the QKV phase's granules
   const unsigned long long* gq = w.gqkv + (long long)b * (p.dim + 2 * p.kv_dim);
   const unsigned long long* srcq = gq + h * HS;
@@ -729,8 +742,8 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
   auto fold = [&](float sc, int n, const float* vrows, int vstride) {
     const float my = lane < n ? __fdiv_rn(sc, rs) : -3.402823466e+38f;
     const float mn = fmaxf(m, wave_max_u(my));
-    const float e = lane < n ? expf_libm(__fsub_rn(my, mn)) : 0.f;
-    const float scale = expf_libm(__fsub_rn(m, mn));
+    const float e = lane < n ? expf_libm_tab(__fsub_rn(my, mn), w.etab) : 0.f;
+    const float scale = expf_libm_tab(__fsub_rn(m, mn), w.etab);
     l = fmaf(l, scale, wave_sum_u(e));
 #pragma unroll
     for (int c = 0; c < VPL; ++c) o[c] *= scale;
@@ -743,20 +756,27 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
   };
   for (int t0 = k0; t0 < ke; t0 += 64) {
     const int n = min(64, ke - t0);
-    if (t0 > k0) {
-      wave_lds_fence();  // the previous round's reads are done before this round lands
-      issue(t0, n);
+    const bool more = t0 + 64 < ke;
+    wait_all_but_round_half();  // this round's K rows (its V rows may still be in flight)
+    const float sc = dot(kw + 4 * lane, 64);
+    wave_lds_fence();  // the K window's reads are done before the next round lands in it
+    if (more) {
+      issue_k(t0 + 64, min(64, ke - t0 - 64));
+      wait_all_but_round_half();  // this round's V rows
+    } else {
+      dma_wait_all();
     }
-    dma_wait_all();
-    fold(dot(kw + 4 * lane, 64), n, vw, HS);
+    fold(sc, n, vw, HS);
+    wave_lds_fence();  // the V window's reads are done
+    if (more) issue_v(t0 + 64, min(64, ke - t0 - 64));
   }
   if (last) {  // key T-1: every lane computes its score (one key), lane 0's counts
     const float sc = dot(kn, 1);
     // fold one key whose V row is vn (in registers): the same arithmetic inline
     const float my = lane < 1 ? __fdiv_rn(sc, rs) : -3.402823466e+38f;
     const float mn = fmaxf(m, wave_max_u(my));
-    const float e0 = expf_libm(__fsub_rn(lane_f(my, 0), mn));
-    const float scale = expf_libm(__fsub_rn(m, mn));
+    const float e0 = expf_libm_tab(__fsub_rn(lane_f(my, 0), mn), w.etab);
+    const float scale = expf_libm_tab(__fsub_rn(m, mn), w.etab);
     l = fmaf(l, scale, e0);
 #pragma unroll
     for (int c = 0; c < VPL; ++c) o[c] = fmaf(e0, vn[c], o[c] * scale);
@@ -794,7 +814,7 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
     for (int c = 0; c < VPL; ++c) ov[k][c] = ld_sc1(recs + kk * (HS + 4) + lane * VPL + c);
   }
   const float M = wave_max_u(lane < nact ? mk : -3.402823466e+38f);
-  const float sk = lane < nact ? expf_libm(__fsub_rn(mk, M)) : 0.f;
+  const float sk = lane < nact ? expf_libm_tab(__fsub_rn(mk, M), w.etab) : 0.f;
   const float L = wave_sum_u(lk * sk);
   float acc[VPL];
 #pragma unroll
