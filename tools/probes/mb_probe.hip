@@ -30,7 +30,7 @@ __device__ __forceinline__ float sel4(const f32x4& a, int i) {
   return i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3];
 }
 
-template <int NR, int NSG, int P, int W, bool NT, bool TILED>
+template <int NR, int NSG, int P, int W, bool NT, bool TILED, bool XG = false>
 __global__ void __launch_bounds__(W * 64) mb_kernel(const float* __restrict__ W0, const float* __restrict__ W1,
                                                     const float* __restrict__ x, int K, int M, int nb, float* y,
                                                     float* part, unsigned* cnt, int maxp) {
@@ -38,7 +38,7 @@ __global__ void __launch_bounds__(W * 64) mb_kernel(const float* __restrict__ W0
   const int C = K >> 6;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nx = C * NSG * 64;
+  const int nx = XG ? 0 : C * NSG * 64;
   for (int e0 = threadIdx.x; e0 < nx; e0 += 8 * W * 64) {  // 8 independent loads in flight per thread
     f4 v[8];
 #pragma unroll
@@ -62,7 +62,11 @@ __global__ void __launch_bounds__(W * 64) mb_kernel(const float* __restrict__ W0
   // issue cursor
   long long ui = u0;
   int rgi = (int)(u0 / C), ci = (int)(u0 - (long long)rgi * C);
-  auto issue = [&](f4 (&w)[NR]) {
+  auto issue = [&](f4 (&w)[NR], f4 (&xg)[NSG]) {
+    if constexpr (XG) {
+#pragma unroll
+      for (int s = 0; s < NSG; ++s) xg[s] = *reinterpret_cast<const f4*>(x + (long long)(4 * s + iq) * K + 64 * ci + 4 * bq);
+    }
     int row = 4 * rgi + iq;
     row = row < M ? row : M - 1;
     const long long off = TILED ? ((long long)rgi * C + ci) * (NR * 256) + 4 * lane : row * Kl + 64 * ci + 4 * bq;
@@ -77,8 +81,9 @@ __global__ void __launch_bounds__(W * 64) mb_kernel(const float* __restrict__ W0
     }
   };
   f4 buf[P][NR];
+  f4 xgb[P][NSG];
 #pragma unroll
-  for (int t = 0; t < P; ++t) issue(buf[t]);
+  for (int t = 0; t < P; ++t) issue(buf[t], xgb[t]);
   f32x4 acc[NR][NSG];
 #pragma unroll
   for (int m = 0; m < NR; ++m)
@@ -93,7 +98,7 @@ __global__ void __launch_bounds__(W * 64) mb_kernel(const float* __restrict__ W0
       if (u < u1) {
         f4 xv[NSG];
 #pragma unroll
-        for (int s = 0; s < NSG; ++s) xv[s] = xl[(cc * NSG + s) * 64 + lane];
+        for (int s = 0; s < NSG; ++s) xv[s] = XG ? xgb[t][s] : xl[(cc * NSG + s) * 64 + lane];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -160,14 +165,14 @@ __global__ void __launch_bounds__(W * 64) mb_kernel(const float* __restrict__ W0
         }
         if (++cc == C) { cc = 0; ++rgc; }
       }
-      issue(buf[t]);
+      issue(buf[t], xgb[t]);
     }
   }
 }
 
 struct Shape { const char* name; int NR, M, K; };
 
-template <int NR, int P, int W, bool NT, bool TILED = false>
+template <int NR, int P, int W, bool NT, bool TILED = false, bool XG = false>
 double run(const Shape& sh, int nb, int grid, const float* Wd, size_t wfl, int ncopy, const float* xd, float* yd,
            float* part, unsigned* cnt, int iters, bool check) {
   const int C = sh.K / 64;
@@ -175,8 +180,8 @@ double run(const Shape& sh, int nb, int grid, const float* Wd, size_t wfl, int n
   const long long NW = (long long)grid * W;
   if (T < NW) return -1;
   const int maxp = (int)((C * NW + T - 1) / T) + 2;
-  const size_t lds = (size_t)C * 2 * 64 * 16;
-  auto kern = mb_kernel<NR, 2, P, W, NT, TILED>;
+  const size_t lds = XG ? 0 : (size_t)C * 2 * 64 * 16;
+  auto kern = mb_kernel<NR, 2, P, W, NT, TILED, XG>;
   CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const size_t mat = (size_t)sh.M * sh.K;
   auto launch = [&](int i) {
@@ -222,14 +227,14 @@ double run(const Shape& sh, int nb, int grid, const float* Wd, size_t wfl, int n
 
 int main(int argc, char** argv) {
   const int nb = argc > 1 ? atoi(argv[1]) : 8;
-  const Shape shapes[] = {{"wo", 1, 4096, 4096}, {"ffn_up", 2, 11008, 4096}, {"cls", 1, 32000, 4096}, {"qkv_as_store", 1, 12288, 4096}};
+  const Shape shapes[] = {{"wo", 1, 4096, 4096}, {"ffn_up", 2, 11008, 4096}, {"cls", 1, 32000, 4096}, {"qkv_as_store", 1, 12288, 4096}, {"ffn_down", 1, 4096, 11008}};
   size_t maxw = 0;
   for (auto& s : shapes) maxw = std::max(maxw, (size_t)s.NR * s.M * s.K);
   float *Wd, *xd, *yd, *part;
   unsigned* cnt;
   const size_t total = (size_t)1600 << 20;  // bytes of weights to rotate over
   CK(hipMalloc(&Wd, total));
-  CK(hipMalloc(&xd, 16 * 4096 * 4));
+  CK(hipMalloc(&xd, 16 * 11008 * 4));
   CK(hipMalloc(&yd, (size_t)2 * 16 * 32000 * 4));
   CK(hipMalloc(&part, (size_t)64 << 20));
   CK(hipMalloc(&cnt, (size_t)1 << 20));
@@ -239,7 +244,7 @@ int main(int argc, char** argv) {
     unsigned s = 12345;
     for (auto& v : h) { s = s * 1664525u + 1013904223u; v = ((int)(s >> 9) - (1 << 22)) * (0.02f / (1 << 22)); }
     CK(hipMemcpy(Wd, h.data(), total, hipMemcpyHostToDevice));
-    std::vector<float> hx(16 * 4096);
+    std::vector<float> hx(16 * 11008);
     for (auto& v : hx) { s = s * 1664525u + 1013904223u; v = ((int)(s >> 9) - (1 << 22)) * (1.0f / (1 << 22)); }
     CK(hipMemcpy(xd, hx.data(), hx.size() * 4, hipMemcpyHostToDevice));
   }
@@ -250,19 +255,24 @@ int main(int argc, char** argv) {
     const int iters = std::max(20, (int)(2e9 / (wfl * 4.0)));
     printf("%s (%.1f MB, %d copies)\n", sh.name, gb * 1e3, ncopy);
 #define RUN(NR_, P_, W_, NT_, G_) RUNT(NR_, P_, W_, NT_, G_, false)
+#define RUNX(NR_, P_, W_, G_, T_)                                                                             \
+    {                                                                                                         \
+      double us = run<NR_, P_, W_, true, T_, true>(sh, nb, G_, Wd, wfl, ncopy, xd, yd, part, cnt, iters, true); \
+      if (us > 0) printf("    NR=%d P=%2d W=%2d grid=%d tiled=%d x-from-L2: %8.2f us  %7.1f GB/s\n", NR_, P_, W_, G_, (int)T_, us, gb / us * 1e6); \
+    }
 #define RUNT(NR_, P_, W_, NT_, G_, T_)                                                                        \
     {                                                                                                         \
       double us = run<NR_, P_, W_, NT_, T_>(sh, nb, G_, Wd, wfl, ncopy, xd, yd, part, cnt, iters, true);       \
       if (us > 0) printf("    NR=%d P=%2d W=%2d NT=%d grid=%d tiled=%d: %8.2f us  %7.1f GB/s\n", NR_, P_, W_, NT_, G_, (int)T_, us, gb / us * 1e6); \
     }
-    if (sh.NR == 1) {
-      RUN(1, 8, 4, true, 256) RUN(1, 8, 8, true, 256) RUN(1, 4, 8, true, 256) RUN(1, 16, 8, true, 256)
-      RUNT(1, 8, 4, true, 256, true) RUNT(1, 16, 4, true, 256, true) RUNT(1, 8, 8, true, 256, true) RUNT(1, 16, 8, true, 256, true)
-      RUNT(1, 16, 8, false, 256, true) RUNT(1, 8, 16, true, 256, true) RUNT(1, 4, 16, true, 256, true)
+    if (sh.K > 4096) {
+      RUNX(1, 8, 8, 256, false) RUNX(1, 8, 8, 512, false) RUNX(1, 8, 4, 512, false) RUNX(1, 8, 4, 1024, false)
+    } else if (sh.NR == 1) {
+      RUN(1, 8, 8, true, 256) RUN(1, 4, 8, true, 256)
+      RUNX(1, 8, 8, 256, false) RUNX(1, 8, 8, 512, false) RUNX(1, 8, 4, 512, false) RUNX(1, 8, 4, 1024, false) RUNX(1, 4, 8, 512, false)
     } else {
-      RUN(2, 8, 4, true, 256) RUN(2, 8, 8, true, 256) RUN(2, 4, 8, true, 256)
-      RUNT(2, 8, 4, true, 256, true) RUNT(2, 16, 4, true, 256, true) RUNT(2, 8, 8, true, 256, true) RUNT(2, 4, 8, true, 256, true)
-      RUNT(2, 8, 8, false, 256, true) RUNT(2, 4, 16, true, 256, true)
+      RUN(2, 8, 8, true, 256) RUN(2, 4, 8, true, 256)
+      RUNX(2, 8, 8, 256, false) RUNX(2, 4, 8, 512, false) RUNX(2, 8, 4, 512, false) RUNX(2, 4, 4, 1024, false)
     }
   }
   return 0;
