@@ -665,7 +665,7 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
   const int kvh = h / p.kv_mul;
   const float* kbase = p.kc + (long long)b * p.kv_b_stride + p.kv_l_off + (long long)kvh * HS;
   const float* vbase = p.vc + (long long)b * p.kv_b_stride + p.kv_l_off + (long long)kvh * HS;
-  float* kw = win;              // [PC][256]: 64 keys transposed
+  float* kw = win;              // [64][HS]: the round's K rows, row-major
   float* vw = kw + 64 * HS;     // [64][HS]
   float* qs = vw + 64 * HS;     // q [HS]
   float* kn = qs + HS;          // k row T-1 [HS]
@@ -674,10 +674,16 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
   // count n (lanes past n re-read row t0 into slots nothing reads), so the waits below can count
   // them: the next round's K rows land while this round's V rows are folded, its V rows while its
   // scores are taken (K and V share no LDS, one window of each).
+  // K rows whole, RPI per wave-instruction (coalesced 1-KiB pieces; a transposed image would
+  // gather 64 rows x 16 B per instruction); the lane-per-key dot below walks its row from piece
+  // `lane` on, so the 16 lanes of a read hit 16 different bank groups
   auto issue_k = [&](int t0, int n) {
-    const float* row = kbase + (long long)(t0 + (lane < n ? lane : 0)) * p.kv_dim;
+    const int kq = lane / PC, pc = lane % PC;
 #pragma unroll
-    for (int i = 0; i < PC; ++i) dma16(row + 4 * i, kw + i * 256);
+    for (int j = 0; j < 64 / RPI; ++j) {
+      const int kl = j * RPI + kq;  // this lane's key in the round
+      dma16(kbase + (long long)(t0 + (kl < n ? kl : 0)) * p.kv_dim + 4 * pc, kw + j * 256);
+    }
   };
   auto issue_v = [&](int t0, int n) {
 #pragma unroll
@@ -758,7 +764,17 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
     const int n = min(64, ke - t0);
     const bool more = t0 + 64 < ke;
     wait_all_but_round_half();  // this round's K rows (its V rows may still be in flight)
-    const float sc = dot(kw + 4 * lane, 64);
+    float sc;
+    {  // key `lane`, pieces in the order lane, lane + 1, ... (mod PC)
+      float a[4] = {0.f, 0.f, 0.f, 0.f};
+      const f4* kr = reinterpret_cast<const f4*>(kw + HS * lane);
+#pragma unroll 8
+      for (int i = 0; i < PC; ++i) {
+        const int pc = (i + lane) & (PC - 1);
+        a[i & 3] = dot4(q4[pc], kr[pc], a[i & 3]);
+      }
+      sc = (a[0] + a[1]) + (a[2] + a[3]);
+    }
     wave_lds_fence();  // the K window's reads are done before the next round lands in it
     if (more) {
       issue_k(t0 + 64, min(64, ke - t0 - 64));
