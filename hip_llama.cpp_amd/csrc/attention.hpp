@@ -670,26 +670,30 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
   float* qs = vw + 64 * HS;     // q [HS]
   float* kn = qs + HS;          // k row T-1 [HS]
   const int ke = min(k1, tc);   // cached keys of this unit: [k0, ke)
-  // A round's K and V rows as exactly PC + 64 / RPI (= 2 PC) wave-instructions whatever its key
-  // count n (lanes past n re-read row t0 into slots nothing reads), so the waits below can count
-  // them: the next round's K rows land while this round's V rows are folded, its V rows while its
-  // scores are taken (K and V share no LDS, one window of each).
+  // Units of more than one 64-key round (long contexts) issue a round's K and V rows as exactly
+  // PC + 64 / RPI (= 2 PC) wave-instructions whatever its key count n (lanes past n re-read row
+  // t0 into slots nothing reads), so the waits below can count them: the next round's K rows land
+  // while this round's V rows are folded, its V rows while its scores are taken (K and V share no
+  // LDS, one window of each).  A single-round unit (short contexts) issues only its n rows.
   // K rows whole, RPI per wave-instruction (coalesced 1-KiB pieces; a transposed image would
   // gather 64 rows x 16 B per instruction); the lane-per-key dot below walks its row from piece
   // `lane` on, so the 16 lanes of a read hit 16 different bank groups
+  const bool multi = ke - k0 > 64;
   auto issue_k = [&](int t0, int n) {
     const int kq = lane / PC, pc = lane % PC;
-#pragma unroll
-    for (int j = 0; j < 64 / RPI; ++j) {
+    const int ni = multi ? 64 / RPI : (n + RPI - 1) / RPI;
+#pragma unroll 4
+    for (int j = 0; j < ni; ++j) {
       const int kl = j * RPI + kq;  // this lane's key in the round
-      dma16(kbase + (long long)(t0 + (kl < n ? kl : 0)) * p.kv_dim + 4 * pc, kw + j * 256);
+      if (multi || kl < n) dma16(kbase + (long long)(t0 + (kl < n ? kl : 0)) * p.kv_dim + 4 * pc, kw + j * 256);
     }
   };
   auto issue_v = [&](int t0, int n) {
-#pragma unroll
-    for (int j = 0; j < 64 / RPI; ++j) {
+    const int ni = multi ? 64 / RPI : (n + RPI - 1) / RPI;
+#pragma unroll 4
+    for (int j = 0; j < ni; ++j) {
       const int r = j * RPI + lane / PC;
-      dma16(vbase + (long long)(t0 + (r < n ? r : 0)) * p.kv_dim + (lane % PC) * 4, vw + j * 256);
+      if (multi || r < n) dma16(vbase + (long long)(t0 + (r < n ? r : 0)) * p.kv_dim + (lane % PC) * 4, vw + j * 256);
     }
   };
   static_assert(64 / RPI == PC, "K and V rounds are the same instruction count");
@@ -763,7 +767,8 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
   for (int t0 = k0; t0 < ke; t0 += 64) {
     const int n = min(64, ke - t0);
     const bool more = t0 + 64 < ke;
-    wait_all_but_round_half();  // this round's K rows (its V rows may still be in flight)
+    if (multi) wait_all_but_round_half();  // this round's K rows (its V rows may still be in flight)
+    else dma_wait_all();
     float sc;
     {  // key `lane`, pieces in the order lane, lane + 1, ... (mod PC)
       float a[4] = {0.f, 0.f, 0.f, 0.f};
