@@ -647,6 +647,9 @@ TL_DEVICE void attn_unit_split(const AttnWaveParams& w, int h, int c, int NG, fl
 // row (T-1, written by this launch's QKV phase) comes from the granules.  Partials combine as in
 // attn_unit (same records and tickets).  win: attn_win_floats(HS) floats of LDS.
 __host__ __device__ constexpr int attn_win_floats(int hs) { return 2 * 64 * hs + 2 * hs; }
+#ifndef ATTN_K_TRANSPOSED
+#define ATTN_K_TRANSPOSED 0
+#endif
 
 template <int HS>
 TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int lane) {
@@ -680,6 +683,13 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
   // `lane` on, so the 16 lanes of a read hit 16 different bank groups
   const bool multi = ke - k0 > 64;
   auto issue_k = [&](int t0, int n) {
+#if ATTN_K_TRANSPOSED  // (A/B: the transposed image, one 16-B piece of 64 rows per instruction)
+    const float* row = kbase + (long long)(t0 + (lane < n ? lane : 0)) * p.kv_dim;
+#pragma unroll 4
+    for (int i = 0; i < PC; ++i)
+      if (multi || lane < n) dma16(row + 4 * i, kw + i * 256);
+    return;
+#endif
     const int kq = lane / PC, pc = lane % PC;
     const int ni = multi ? 64 / RPI : (n + RPI - 1) / RPI;
 #pragma unroll 4
@@ -770,6 +780,9 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
     if (multi) wait_all_but_round_half();  // this round's K rows (its V rows may still be in flight)
     else dma_wait_all();
     float sc;
+#if ATTN_K_TRANSPOSED
+    sc = dot(kw + 4 * lane, 64);
+#else
     {  // key `lane`, pieces in the order lane, lane + 1, ... (mod PC)
       float a[4] = {0.f, 0.f, 0.f, 0.f};
       const f4* kr = reinterpret_cast<const f4*>(kw + HS * lane);
@@ -780,6 +793,7 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
       }
       sc = (a[0] + a[1]) + (a[2] + a[3]);
     }
+#endif
     wave_lds_fence();  // the K window's reads are done before the next round lands in it
     if (more) {
       issue_k(t0 + 64, min(64, ke - t0 - 64));
