@@ -18,7 +18,9 @@
 // inside a step, so a step can be captured into a hipGraph.
 #include <math.h>
 #include <string.h>
+#include <atomic>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <tuple>
 #include <vector>
@@ -32,6 +34,7 @@
 #include "q8_dispatch.hpp"
 #include "persist.hpp"
 #include "prefill.hpp"
+#include "api_lock.hpp"
 
 using tl::f4;
 
@@ -47,6 +50,15 @@ extern "C" const char* thallama_last_error(void) { return g_last_error.c_str(); 
       return (int)e_;                                                                 \
     }                                                                                 \
   } while (0)
+
+// ------------------------------------------------------------------ concurrent callers
+// Every per-call operation of a decoder is ordered on its own non-blocking stream (async copies
+// and memsets + hipStreamSynchronize; workspaces allocated at creation).  What must stay
+// device-wide — allocation, frees and zeroing at create/destroy, the diagnostics' one-time buffers,
+// kernel attributes — and every capture (begin .. instantiate) run under tl::api_mu()
+// (api_lock.hpp), so no such call can fall inside another thread's capture.
+using tl::ApiLock;
+using tl::api_mu;
 
 // ------------------------------------------------------------------ argmax + advance
 // next = argmax(logits[b]) with lowest-index ties (sample_argmax, reference
@@ -107,6 +119,9 @@ __global__ void __launch_bounds__(1024) k_argmax_advance(const float* logits, in
 
 // ------------------------------------------------------------------ decoder
 static constexpr int kAttnChunk = 32;  // keys per attention wave unit
+// batched prefill (thallama_decoder_prefill): tokens per chunk and attention splits per token
+static constexpr int kPrefillChunk = 128;
+static constexpr int kPrefillMaxSplits = 16;
 
 struct thallama_decoder {
   Config cfg;
@@ -124,6 +139,8 @@ struct thallama_decoder {
   int* tok_h = nullptr;  // pinned staging
   int* pos_h = nullptr;
   int* nxt_h = nullptr;  // pinned: argmax ids of a greedy step
+  unsigned* perr_h = nullptr;  // pinned: the persistent step's error word, read back on d->stream
+  bool err_pending = false;    // perr_h holds the word of launches not yet checked
   float2* rope_d = nullptr;
   float* xn_d = nullptr;        // [<=16][dim] normed rows for the matrix-core GEMV (batch >= 2)
   float* ssq_d = nullptr;       // [B][dim/16] per-tile sums of squares carried from Wo / W2 to the next norm
@@ -166,11 +183,12 @@ struct thallama_decoder {
   bool pok = false;             // shape supported
   unsigned long long* ptrace = nullptr;  // optional timeline of the persistent step
   size_t ptrace_n = 0;
-  // batched prompt processing (prefill.hip), allocated on first use for kPrefillChunk tokens
+  // batched prompt processing (prefill.hip) for kPrefillChunk tokens, allocated at creation
   float *pf_x = nullptr, *pf_xn = nullptr, *pf_q = nullptr, *pf_xb = nullptr, *pf_hb = nullptr;
   float* pf_part = nullptr;
   unsigned* pf_cnt = nullptr;
   int *pf_tok = nullptr, *pf_pos = nullptr;
+  int* pf_tok_h = nullptr;      // pinned staging of a chunk's prompt tokens
   std::string pwhy;             // why not
   // profiling
   std::vector<hipEvent_t> ev_pool;
@@ -272,6 +290,11 @@ static int batch_persist_default_max() {
   return v;
 }
 
+// Shapes the batched prefill handles (head size 64/128/256, rows in multiples of 32).
+static bool prefill_shape_ok(const thallama_decoder* d) {
+  return (d->hs == 64 || d->hs == 128 || d->hs == 256) && d->dim % 32 == 0 && d->hidden % 32 == 0;
+}
+
 extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg, const TransformerWeights* w,
                                        const RunState* s, int batch, hipStream_t stream) {
   if (!out || !cfg || !w || !s || batch <= 0) {
@@ -300,6 +323,7 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
   d->kv_mul = c.n_heads / c.n_kv_heads;
   d->V = d->cfg.vocab_size;
   d->S = c.seq_len;
+  ApiLock lock(api_mu());
   TL_TRY(hipGetDevice(&d->dev));
   if (stream) {
     d->stream = stream;
@@ -371,6 +395,28 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
     }
     if (!d->pok && why) d->pwhy = why;
   }
+  if (!d->mpart_d) {  // split-K scratch of the matrix-core GEMV (batch 1: prefill's short chunks)
+    const size_t nblk = (size_t)tl::mfma_target_blocks();
+    TL_TRY(hipMalloc(&d->mpart_d, sizeof(float) * nblk * 2 * 256));
+    TL_TRY(hipMalloc(&d->mcnt_d, sizeof(unsigned) * nblk));
+    TL_TRY(hipMemset(d->mcnt_d, 0, sizeof(unsigned) * nblk));
+  }
+  TL_TRY(hipHostMalloc(&d->perr_h, sizeof(unsigned), hipHostMallocDefault));
+  *d->perr_h = 0;
+  if (prefill_shape_ok(d)) {  // batched prompt processing (thallama_decoder_prefill)
+    const size_t CH = kPrefillChunk, dim = d->dim, hid = d->hidden;
+    TL_TRY(hipMalloc(&d->pf_x, sizeof(float) * CH * dim));
+    TL_TRY(hipMalloc(&d->pf_xn, sizeof(float) * CH * (dim > hid ? dim : hid)));
+    TL_TRY(hipMalloc(&d->pf_q, sizeof(float) * CH * dim));
+    TL_TRY(hipMalloc(&d->pf_xb, sizeof(float) * CH * dim));
+    TL_TRY(hipMalloc(&d->pf_hb, sizeof(float) * CH * hid));
+    TL_TRY(hipMalloc(&d->pf_part, sizeof(float) * CH * d->H * kPrefillMaxSplits * (d->hs + 4)));
+    TL_TRY(hipMalloc(&d->pf_cnt, sizeof(unsigned) * CH * d->H));
+    TL_TRY(hipMemset(d->pf_cnt, 0, sizeof(unsigned) * CH * d->H));
+    TL_TRY(hipMalloc(&d->pf_tok, sizeof(int) * (size_t)d->S));
+    TL_TRY(hipMalloc(&d->pf_pos, sizeof(int) * CH));
+    TL_TRY(hipHostMalloc(&d->pf_tok_h, sizeof(int) * (size_t)d->S, hipHostMallocDefault));
+  }
   if (d->pok) {
     d->psync_zero = tl::kPSyncWords + (((size_t)d->L * d->H * batch + 3) & ~(size_t)3);
     TL_TRY(hipMalloc(&d->psync, sizeof(unsigned) * (d->psync_zero + 32)));
@@ -387,6 +433,7 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
 extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   if (!d) return;
   (void)hipStreamSynchronize(d->stream);
+  ApiLock lock(api_mu());
   drop_graphs(d);
   for (auto e : d->ev_pool) (void)hipEventDestroy(e);
   (void)hipFree(d->tok_d);
@@ -395,6 +442,8 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   (void)hipHostFree(d->tok_h);
   (void)hipHostFree(d->pos_h);
   (void)hipHostFree(d->nxt_h);
+  (void)hipHostFree(d->perr_h);
+  (void)hipHostFree(d->pf_tok_h);
   (void)hipFree(d->rope_d);
   (void)hipFree(d->xn_d);
   (void)hipFree(d->ssq_d);
@@ -776,16 +825,30 @@ static int enqueue_persistent(thallama_decoder* d, bool argmax) {
 // (every K/V row the failed call wrote is rewritten, in order, before it is read again).
 constexpr int kPersistFellBack = (int)hipErrorLaunchFailure;
 
+// Enqueued on d->stream after a call's persistent launches, before its synchronisation: the
+// error word lands in pinned host memory with the rest of the call (no legacy-stream copy).
+static int enqueue_err_read(thallama_decoder* d) {
+  if (!d->psync || !use_persist(d)) return 0;
+  TL_TRY(hipMemcpyAsync(d->perr_h, d->psync + d->psync_zero, sizeof(unsigned), hipMemcpyDeviceToHost, d->stream));
+  d->err_pending = true;
+  return 0;
+}
+
+// After the synchronisation that covered enqueue_err_read.
 static int check_persist(thallama_decoder* d) {
-  if (!d->psync) return 0;
-  unsigned err = 0;
-  TL_TRY(hipMemcpy(&err, d->psync + d->psync_zero, sizeof(unsigned), hipMemcpyDeviceToHost));
-  if (!err) return 0;
-  TL_TRY(hipMemset(d->psync, 0, sizeof(unsigned) * (d->psync_zero + 32)));
-  TL_TRY(hipMemset(d->cnt_d, 0, sizeof(unsigned) * (size_t)d->B * d->H));
+  if (!d->err_pending) return 0;
+  d->err_pending = false;
+  if (!*d->perr_h) return 0;
+  *d->perr_h = 0;
+  TL_TRY(hipMemsetAsync(d->psync, 0, sizeof(unsigned) * (d->psync_zero + 32), d->stream));
+  TL_TRY(hipMemsetAsync(d->cnt_d, 0, sizeof(unsigned) * (size_t)d->B * d->H, d->stream));
+  TL_TRY(hipStreamSynchronize(d->stream));
   d->pok = false;
   d->pwhy = "a grid barrier timed out";
-  drop_graphs(d);  // the captured graphs hold the persistent launch
+  {
+    ApiLock lock(api_mu());
+    drop_graphs(d);  // the captured graphs hold the persistent launch
+  }
   g_last_error = "persistent step: a grid barrier timed out (grid not co-resident); path disabled";
   return kPersistFellBack;
 }
@@ -799,8 +862,8 @@ extern "C" int thallama_decoder_granules(thallama_decoder* d, unsigned long long
   if (!d || !d->pgran) return (int)hipErrorInvalidValue;
   const size_t ng = granule_count(d);
   if (!host) return (int)ng;
+  TL_TRY(hipMemcpyAsync(host, d->pgran, (n < ng ? n : ng) * 8, hipMemcpyDeviceToHost, d->stream));
   TL_TRY(hipStreamSynchronize(d->stream));
-  TL_TRY(hipMemcpy(host, d->pgran, (n < ng ? n : ng) * 8, hipMemcpyDeviceToHost));
   return (int)ng;
 }
 
@@ -810,15 +873,16 @@ extern "C" int thallama_decoder_ptrace(thallama_decoder* d, int enable, unsigned
   if (!d) return (int)hipErrorInvalidValue;
   const size_t need = (size_t)d->ncu * (5 * d->L + 1) * tl::kTraceSlots;
   if (enable && !d->ptrace) {
+    ApiLock lock(api_mu());
     TL_TRY(hipMalloc(&d->ptrace, need * sizeof(unsigned long long)));
-    TL_TRY(hipMemset(d->ptrace, 0, need * sizeof(unsigned long long)));
+    TL_TRY(hipMemsetAsync(d->ptrace, 0, need * sizeof(unsigned long long), d->stream));
     d->ptrace_n = need;
     drop_graphs(d);
   }
   if (host && d->ptrace) {
+    TL_TRY(hipMemcpyAsync(host, d->ptrace, (n < d->ptrace_n ? n : d->ptrace_n) * sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost, d->stream));
     TL_TRY(hipStreamSynchronize(d->stream));
-    TL_TRY(hipMemcpy(host, d->ptrace, (n < d->ptrace_n ? n : d->ptrace_n) * sizeof(unsigned long long),
-                     hipMemcpyDeviceToHost));
   }
   return (int)need;
 }
@@ -881,6 +945,7 @@ static int decoder_forward_once(thallama_decoder* d, const int* token_h, const i
   if (r) return r;
   if (d->use_graph && !d->profile) {  // the step (~160 launches at batch > 1) replayed as one graph
     if (!d->exec_fwd) {
+      ApiLock lock(api_mu());
       hipGraph_t g = nullptr;
       TL_TRY(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
       const int e = use_persist(d) ? enqueue_persistent(d, false) : enqueue_step(d);
@@ -898,6 +963,7 @@ static int decoder_forward_once(thallama_decoder* d, const int* token_h, const i
   if (logits_h)
     TL_TRY(hipMemcpyAsync(logits_h, d->s.logits, sizeof(float) * (size_t)d->B * d->V, hipMemcpyDeviceToHost,
                           d->stream));
+  if ((r = enqueue_err_read(d)) != 0) return r;
   TL_TRY(hipStreamSynchronize(d->stream));
   prof_collect(d);
   return check_persist(d);
@@ -909,6 +975,7 @@ static int decoder_greedy_once(thallama_decoder* d, const int* token0_h, const i
 // One greedy step (the step + the argmax that feeds tok/pos) captured as a graph, once.
 static int ensure_greedy_graph(thallama_decoder* d) {
   if (d->exec) return 0;
+  ApiLock lock(api_mu());
   hipGraph_t g = nullptr;
   TL_TRY(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
   int e = 0;
@@ -941,6 +1008,7 @@ static int decoder_step_argmax_once(thallama_decoder* d, const int* token_h, con
     if (r) return r;
   }
   TL_TRY(hipMemcpyAsync(d->nxt_h, d->tok_d, sizeof(int) * d->B, hipMemcpyDeviceToHost, d->stream));
+  if ((r = enqueue_err_read(d)) != 0) return r;
   TL_TRY(hipStreamSynchronize(d->stream));
   memcpy(next_h, d->nxt_h, sizeof(int) * d->B);
   prof_collect(d);
@@ -996,6 +1064,7 @@ static int decoder_greedy_once(thallama_decoder* d, const int* token0_h, const i
       if (r) return r;
     }
   }
+  if (n_steps > 0 && (r = enqueue_err_read(d)) != 0) return r;
   if (tokens_out_h && n_steps > 0) {
     // tokens by position: sequence b generated out[b][pos0+1 .. pos0+n_steps] ... stored at pos index
     std::vector<int> tmp((size_t)d->B * d->S);
@@ -1091,21 +1160,32 @@ extern "C" double thallama_step_bytes(const Config* c, int B, int kclass, const 
 // ------------------------------------------------------------------ thaDNN_s_forward_batch
 // The reference signature carries no workspace, so a decoder per (device, stream, batch, config,
 // fp32|int8) is created on first use and reused.  A call with other weight / state buffers than
-// the cached decoder's replaces it (the old one and its workspace are freed), and at most
-// kDecCacheMax decoders live at once (least recently used evicted), so a host that reallocates
-// its buffers does not grow without bound.  thallama_forward_batch_cache_size() reports the count.
+// the cached decoder's replaces it, and at most kDecCacheMax decoders stay cached (least recently
+// used evicted), so a host that reallocates its buffers does not grow without bound.
+// The reference calls this entry from one host thread per GPU (src/llama.cpp:919, 1017), so
+// entries are shared: a caller holds a reference (shared_ptr) for the whole forward, eviction only
+// drops the cache's reference, and the decoder is destroyed when its last user returns; callers
+// of one entry are serialised by its mutex.  thallama_forward_batch_cache_size() reports the count.
 namespace {
 typedef std::tuple<int, hipStream_t, int, int, int, int, int, int, int, int> DecKey;
+struct CachedDecoder {
+  thallama_decoder* d = nullptr;
+  std::mutex use;           // one forward at a time per decoder
+  TransformerWeights w{};   // fp32 buffers the decoder was made for
+  Q8TransformerWeights w8{};  // (int8)
+  RunState s{};
+  ~CachedDecoder() {
+    if (d) thallama_decoder_destroy(d);
+  }
+};
 struct DecEntry {
-  thallama_decoder* d;
+  std::shared_ptr<CachedDecoder> c;
   unsigned long long used;
-  TransformerWeights w;     // fp32 buffers the decoder was made for
-  Q8TransformerWeights w8;  // (int8)
-  RunState s;
 };
 constexpr size_t kDecCacheMax = 8;
 std::mutex g_dec_mu;
 unsigned long long g_dec_clock = 0;
+std::atomic<long long> g_dec_live{0};  // decoders alive (cached or still in use after eviction)
 std::map<DecKey, DecEntry>& dec_cache() {
   static std::map<DecKey, DecEntry> m;
   return m;
@@ -1113,38 +1193,39 @@ std::map<DecKey, DecEntry>& dec_cache() {
 
 // The cached decoder for key, if it was made for exactly these buffers; else a new one (replacing
 // a stale entry, evicting the least recently used beyond the cap).  Caller holds g_dec_mu.
-thallama_decoder* dec_lookup(const DecKey& key, const Config* p, const TransformerWeights* w,
-                             const Q8TransformerWeights* w8, const RunState* s, int B, hipStream_t st) {
+std::shared_ptr<CachedDecoder> dec_lookup(const DecKey& key, const Config* p, const TransformerWeights* w,
+                                          const Q8TransformerWeights* w8, const RunState* s, int B, hipStream_t st) {
   auto& m = dec_cache();
   auto it = m.find(key);
   if (it != m.end()) {
-    DecEntry& e = it->second;
+    CachedDecoder& e = *it->second.c;
     const bool same = memcmp(&e.s, s, sizeof(RunState)) == 0 &&
                       (w8 ? memcmp(&e.w8, w8, sizeof(*w8)) == 0 : memcmp(&e.w, w, sizeof(*w)) == 0);
     if (same) {
-      e.used = ++g_dec_clock;
-      return e.d;
+      it->second.used = ++g_dec_clock;
+      return it->second.c;
     }
-    thallama_decoder_destroy(e.d);
-    m.erase(it);
+    m.erase(it);  // destroyed now, or when its last user returns
   }
   while (m.size() >= kDecCacheMax) {
     auto lru = m.begin();
     for (auto i = m.begin(); i != m.end(); ++i)
       if (i->second.used < lru->second.used) lru = i;
-    thallama_decoder_destroy(lru->second.d);
     m.erase(lru);
   }
   thallama_decoder* d = nullptr;
   const int r = w8 ? thallama_decoder_create_q8(&d, p, w8, s, B, st) : thallama_decoder_create(&d, p, w, s, B, st);
   if (r != 0) return nullptr;
-  DecEntry e = {};
-  e.d = d;
-  e.used = ++g_dec_clock;
-  if (w8) e.w8 = *w8; else e.w = *w;
-  e.s = *s;
-  m[key] = e;
-  return d;
+  std::shared_ptr<CachedDecoder> c(new CachedDecoder(), [](CachedDecoder* x) {
+    delete x;
+    --g_dec_live;
+  });
+  ++g_dec_live;
+  c->d = d;
+  if (w8) c->w8 = *w8; else c->w = *w;
+  c->s = *s;
+  m[key] = DecEntry{c, ++g_dec_clock};
+  return c;
 }
 }  // namespace
 
@@ -1153,10 +1234,34 @@ extern "C" int thallama_forward_batch_cache_size(void) {
   return (int)dec_cache().size();
 }
 
+// Decoders alive: the cached ones plus evicted ones a caller is still running.
+extern "C" int thallama_forward_batch_live(void) { return (int)g_dec_live.load(); }
+
 extern "C" void thallama_forward_batch_cache_clear(void) {
-  std::lock_guard<std::mutex> g(g_dec_mu);
-  for (auto& kv : dec_cache()) thallama_decoder_destroy(kv.second.d);
-  dec_cache().clear();
+  std::map<DecKey, DecEntry> gone;
+  {
+    std::lock_guard<std::mutex> g(g_dec_mu);
+    gone.swap(dec_cache());
+  }
+  // (destroyed here, outside the lock, unless a caller still holds one)
+}
+
+// Runs f(decoder) with the decoder for (key, buffers) pinned and its use lock held.
+template <class F>
+static int with_cached_decoder(const DecKey& key, const Config* p, const TransformerWeights* w,
+                               const Q8TransformerWeights* w8, const RunState* s, int B, hipStream_t st,
+                               const char* who, F f) {
+  std::shared_ptr<CachedDecoder> c;
+  {
+    std::lock_guard<std::mutex> g(g_dec_mu);
+    c = dec_lookup(key, p, w, w8, s, B, st);
+  }
+  if (!c) {
+    fprintf(stderr, "%s: %s\n", who, thallama_last_error());
+    return (int)hipErrorInvalidValue;
+  }
+  std::lock_guard<std::mutex> use(c->use);
+  return f(c->d);
 }
 
 extern "C" thablasStatus_t thaDNN_s_forward_batch(thablasHandle_t handle1, thablasHandle_t handle2,
@@ -1170,28 +1275,21 @@ extern "C" thablasStatus_t thaDNN_s_forward_batch(thablasHandle_t handle1, thabl
   CHECK_HIP(hipGetDevice(&dev));
   DecKey key(dev, handle1.calc_stream, n_batches, p->dim, p->hidden_dim, p->n_layers, p->n_heads, p->n_kv_heads,
              p->seq_len, p->vocab_size);
-  thallama_decoder* d = nullptr;
-  {
-    std::lock_guard<std::mutex> g(g_dec_mu);
-    d = dec_lookup(key, p, w, nullptr, s_batch, n_batches, handle1.calc_stream);
-    if (!d) {
-      fprintf(stderr, "thaDNN_s_forward_batch: %s\n", thallama_last_error());
-      return THABLAS_STATUS_INVALID_VALUE;
-    }
-  }
-  // The reference's scheduler (src/llama.cpp:961-1017) runs every slot of the batch, and a slot
-  // that never received a request carries uninitialised token/pos; its kernel would read out of
-  // bounds.  Such slots run as token 0 at position 0 here: they write only their own K/V row 0,
-  // which a request later admitted to the slot rewrites at its first step, and their logits are
-  // never read.
-  std::vector<int> tk(token, token + n_batches), ps(pos, pos + n_batches);
-  for (int b = 0; b < n_batches; ++b)
-    if (tk[b] < 0 || tk[b] >= d->V || ps[b] < 0 || ps[b] >= d->S) tk[b] = ps[b] = 0;
-  int r = thallama_decoder_forward(d, tk.data(), ps.data(), logits_host);
-  if (r) {
-    fprintf(stderr, "thaDNN_s_forward_batch: %s\n", thallama_last_error());
-    return r == (int)hipErrorInvalidValue ? THABLAS_STATUS_INVALID_VALUE : THABLAS_STATUS_EXECUTION_FAILED;
-  }
+  const int r = with_cached_decoder(
+      key, p, w, nullptr, s_batch, n_batches, handle1.calc_stream, "thaDNN_s_forward_batch", [&](thallama_decoder* d) {
+        // The reference's scheduler (src/llama.cpp:961-1017) runs every slot of the batch, and a
+        // slot that never received a request carries uninitialised token/pos; its kernel would
+        // read out of bounds.  Such slots run as token 0 at position 0 here: they write only their
+        // own K/V row 0, which a request later admitted to the slot rewrites at its first step,
+        // and their logits are never read.
+        std::vector<int> tk(token, token + n_batches), ps(pos, pos + n_batches);
+        for (int b = 0; b < n_batches; ++b)
+          if (tk[b] < 0 || tk[b] >= d->V || ps[b] < 0 || ps[b] >= d->S) tk[b] = ps[b] = 0;
+        const int e = thallama_decoder_forward(d, tk.data(), ps.data(), logits_host);
+        if (e) fprintf(stderr, "thaDNN_s_forward_batch: %s\n", thallama_last_error());
+        return e;
+      });
+  if (r) return r == (int)hipErrorInvalidValue ? THABLAS_STATUS_INVALID_VALUE : THABLAS_STATUS_EXECUTION_FAILED;
   return THABLAS_STATUS_SUCCESS;
 }
 
@@ -1228,6 +1326,7 @@ extern "C" int thallama_decoder_create_q8(thallama_decoder** out, const Config* 
   w.rms_att_weight = w8->rms_att_weight;
   w.rms_ffn_weight = w8->rms_ffn_weight;
   w.rms_final_weight = w8->rms_final_weight;
+  ApiLock lock(api_mu());
   const int r = thallama_decoder_create(out, cfg, &w, s, batch, stream);
   if (r) return r;
   thallama_decoder* d = *out;
@@ -1239,6 +1338,7 @@ extern "C" int thallama_decoder_create_q8(thallama_decoder** out, const Config* 
     d->q8x = !(e && e[0] == '0') && batch <= 8 && tl::q8_exact_ok(w8->group_size, d->dim, d->hidden, d->hs, d->S);
   }
   if (d->q8x) {
+    TL_TRY(tl::q8_exact_prepare());  // the kernels' dynamic-LDS limit, once per device
     TL_TRY(hipMalloc(&d->q8att_d, sizeof(float) * (size_t)batch * d->H * d->S));
     if (batch < 2) {  // (batch 1 multi-launch: the quantised activations' scratch too)
       const size_t kmax = (size_t)(d->dim > d->hidden ? d->dim : d->hidden);
@@ -1309,20 +1409,13 @@ extern "C" thablasStatus_t thaDNN_q8_forward_batch(thablasHandle_t handle, int n
   CHECK_HIP(hipGetDevice(&dev));
   DecKey key(dev, handle.calc_stream, n_batches, p->dim, p->hidden_dim, p->n_layers, p->n_heads, p->n_kv_heads,
              p->seq_len, -(p->vocab_size < 0 ? -p->vocab_size : p->vocab_size) - 1 /* int8 keyspace */);
-  thallama_decoder* d = nullptr;
-  {
-    std::lock_guard<std::mutex> g(g_dec_mu);
-    d = dec_lookup(key, p, nullptr, w, s_batch, n_batches, handle.calc_stream);
-    if (!d) {
-      fprintf(stderr, "thaDNN_q8_forward_batch: %s\n", thallama_last_error());
-      return THABLAS_STATUS_INVALID_VALUE;
-    }
-  }
-  const int r = thallama_decoder_forward(d, token, pos, logits_host);
-  if (r) {
-    fprintf(stderr, "thaDNN_q8_forward_batch: %s\n", thallama_last_error());
-    return r == (int)hipErrorInvalidValue ? THABLAS_STATUS_INVALID_VALUE : THABLAS_STATUS_EXECUTION_FAILED;
-  }
+  const int r = with_cached_decoder(key, p, nullptr, w, s_batch, n_batches, handle.calc_stream,
+                                    "thaDNN_q8_forward_batch", [&](thallama_decoder* d) {
+                                      const int e = thallama_decoder_forward(d, token, pos, logits_host);
+                                      if (e) fprintf(stderr, "thaDNN_q8_forward_batch: %s\n", thallama_last_error());
+                                      return e;
+                                    });
+  if (r) return r == (int)hipErrorInvalidValue ? THABLAS_STATUS_INVALID_VALUE : THABLAS_STATUS_EXECUTION_FAILED;
   return THABLAS_STATUS_SUCCESS;
 }
 
@@ -1331,8 +1424,6 @@ extern "C" thablasStatus_t thaDNN_q8_forward_batch(thablasHandle_t handle, int n
 // projection for up to kPrefillChunk tokens, the decode attention kernel over the chunk's
 // positions, K/V rows written at pos0.. of sequence b.  No logits: the caller's next decode
 // step starts from the token after the prefilled ones.  fp32 weights, head size 64/128/256.
-static constexpr int kPrefillChunk = 128;
-
 // A prefill projection.  Up to kPrefillGemvMax tokens the decode GEMV (matrix cores from 4
 // tokens on: gemv_mfma.hpp, ~4.5 TB/s) beats the GEMM, whose grid is only M/128 blocks at
 // one 64-token tile (7B: 32-172 blocks, ~1 TB/s); the same epilogues either way.
@@ -1340,13 +1431,6 @@ static constexpr int kPrefillGemvMax = 16;
 static constexpr int kPrefillGemmMin = 80;
 static hipError_t prefill_proj(thallama_decoder* d, int mode, const tl::PGemmArgs& g, long long kv_l_off) {
   if (g.n > kPrefillGemvMax) return tl::prefill_gemm(mode, g, d->stream);
-  if (!d->mpart_d) {  // split-K scratch of the matrix-core GEMV (decoders of batch >= 2 have it)
-    const size_t nblk = (size_t)tl::mfma_target_blocks();
-    hipError_t e = hipMalloc(&d->mpart_d, sizeof(float) * nblk * 2 * 256);
-    if (e == hipSuccess) e = hipMalloc(&d->mcnt_d, sizeof(unsigned) * nblk);
-    if (e == hipSuccess) e = hipMemset(d->mcnt_d, 0, sizeof(unsigned) * nblk);
-    if (e != hipSuccess) return e;
-  }
   tl::GemvParams p = {};
   p.W0 = g.W0; p.W1 = g.W1; p.W2 = g.W2;
   p.K = g.K;
@@ -1371,7 +1455,7 @@ extern "C" int thallama_decoder_prefill(thallama_decoder* d, int b, const int* t
     return (int)hipErrorInvalidValue;
   }
   if (n == 0) return 0;
-  if (d->q8 || (d->hs != 64 && d->hs != 128 && d->hs != 256) || d->dim % 32 || d->hidden % 32) {
+  if (d->q8 || !prefill_shape_ok(d)) {
     g_last_error = "thallama_decoder_prefill: unsupported (int8 weights, or head size not 64/128/256)";
     return (int)hipErrorNotSupported;
   }
@@ -1381,24 +1465,19 @@ extern "C" int thallama_decoder_prefill(thallama_decoder* d, int b, const int* t
       return (int)hipErrorInvalidValue;
     }
   const int CH = kPrefillChunk, dim = d->dim, hid = d->hidden, kvd = d->kv_dim, S = d->S;
-  const int max_ns = 16;
+  const int max_ns = kPrefillMaxSplits;
   if (!d->pf_x) {
-    TL_TRY(hipMalloc(&d->pf_x, sizeof(float) * (size_t)CH * dim));
-    TL_TRY(hipMalloc(&d->pf_xn, sizeof(float) * (size_t)CH * (dim > hid ? dim : hid)));
-    TL_TRY(hipMalloc(&d->pf_q, sizeof(float) * (size_t)CH * dim));
-    TL_TRY(hipMalloc(&d->pf_xb, sizeof(float) * (size_t)CH * dim));
-    TL_TRY(hipMalloc(&d->pf_hb, sizeof(float) * (size_t)CH * hid));
-    TL_TRY(hipMalloc(&d->pf_part, sizeof(float) * (size_t)CH * d->H * max_ns * (d->hs + 4)));
-    TL_TRY(hipMalloc(&d->pf_cnt, sizeof(unsigned) * (size_t)CH * d->H));
-    TL_TRY(hipMemset(d->pf_cnt, 0, sizeof(unsigned) * (size_t)CH * d->H));
-    TL_TRY(hipMalloc(&d->pf_tok, sizeof(int) * CH));
-    TL_TRY(hipMalloc(&d->pf_pos, sizeof(int) * CH));
+    g_last_error = "thallama_decoder_prefill: no prefill workspace";
+    return (int)hipErrorNotSupported;
   }
   const TransformerWeights& w = d->w;
   const long long kv_b_stride = (long long)d->L * S * kvd;
   float* kc_b = d->s.key_cache + (long long)b * kv_b_stride;
   float* vc_b = d->s.value_cache + (long long)b * kv_b_stride;
   hipStream_t st = d->stream;
+  // the prompt's ids through pinned staging (the previous call ended with a synchronisation)
+  memcpy(d->pf_tok_h, tokens_h, sizeof(int) * n);
+  TL_TRY(hipMemcpyAsync(d->pf_tok, d->pf_tok_h, sizeof(int) * n, hipMemcpyHostToDevice, st));
   for (int c = 0, m = 0; c < n; c += m) {
     // GEMM chunks of up to CH tokens; a rest of at most kPrefillGemmMin tokens goes through
     // the decode GEMV 16 tokens at a time (about 6 ms per 16 at 7B, against a GEMM floor of
@@ -1406,9 +1485,8 @@ extern "C" int thallama_decoder_prefill(thallama_decoder* d, int b, const int* t
     const int rest = n - c;
     m = rest > kPrefillGemmMin ? (rest < CH ? rest : CH) : (rest < kPrefillGemvMax ? rest : kPrefillGemvMax);
     const int p0 = pos0 + c;
-    TL_TRY(hipMemcpyAsync(d->pf_tok, tokens_h + c, sizeof(int) * m, hipMemcpyHostToDevice, st));
     TL_TRY(tl::prefill_positions(d->pf_pos, p0, m, st));
-    TL_TRY(tl::prefill_embed(d->pf_x, w.token_embedding_table, d->pf_tok, m, dim, st));
+    TL_TRY(tl::prefill_embed(d->pf_x, w.token_embedding_table, d->pf_tok + c, m, dim, st));
     for (int l = 0; l < d->L; ++l) {
       const long long ll = l;
       tl::PGemmArgs g = {};

@@ -11,6 +11,7 @@
 #include "gemv_q8.hpp"
 #include "gemv_q8_mfma.hpp"
 #include "q8_dispatch.hpp"
+#include "api_lock.hpp"
 
 namespace tl {
 
@@ -324,6 +325,7 @@ __global__ void __launch_bounds__(256) k_dequant(float* out, const int8_t* q, co
 extern "C" int thallama_q8_dequant_embedding(const Q8TransformerWeights* w, const Config* p, hipStream_t stream) {
   if (!w || !p || !w->token_embedding_table) return (int)hipErrorInvalidValue;
   const size_t n = (size_t)(p->vocab_size < 0 ? -p->vocab_size : p->vocab_size) * p->dim;
+  tl::ApiLock lock(tl::api_mu());  // (the legacy stream when stream is null: api_lock.hpp)
   hipLaunchKernelGGL(k_dequant, dim3(4096), dim3(256), 0, stream, w->token_embedding_table, w->q_tokens[0].q,
                      w->q_tokens[0].s, n, w->group_size);
   return (int)hipGetLastError();
@@ -347,6 +349,7 @@ extern "C" int thallama_q8_quantize_model(void* payload, const TransformerWeight
   const size_t L = p->n_layers, dim = p->dim, kvd = (size_t)p->dim * p->n_kv_heads / p->n_heads;
   const size_t hid = p->hidden_dim, V = p->vocab_size < 0 ? -p->vocab_size : p->vocab_size;
   unsigned char* ptr = (unsigned char*)payload;
+  tl::ApiLock lock(tl::api_mu());  // (the legacy stream when stream is null: api_lock.hpp)
   hipError_t e;
   if ((e = hipMemcpyAsync(ptr, w->rms_att_weight, 4 * L * dim, hipMemcpyDeviceToDevice, stream))) return (int)e;
   ptr += 4 * L * dim;

@@ -12,6 +12,8 @@ bool q8_swiglu_quant_ok(int nb, int gs, int K, int n_items);
 // GEMV (quantises its input first unless p.xq_ready; p.xq / p.xqs scratch required) and the
 // attention (scores through att [B][H][S], output fp32 into a.out).
 bool q8_exact_ok(int gs, int dim, int hidden, int hs, int seq_len);
+// Kernel attributes of the exact int8 launches on the current device (decoder creation).
+hipError_t q8_exact_prepare();
 hipError_t launch_gemv_q8_exact(int mode, const GemvParams& p, hipStream_t stream, bool nt);
 struct AttnParams;
 hipError_t launch_attn_q8_exact(const AttnParams& a, int B, float* att, hipStream_t stream);

@@ -32,23 +32,6 @@
 
 namespace tl {
 
-// Raise a kernel's dynamic-LDS limit to 160 KiB on the current device, once per (kernel, device):
-// the attribute is per device, and the CLI creates decoders on several devices from several
-// threads (app/run.cpp).
-static hipError_t lds_attr(const void* fn) {
-  static std::mutex mu;
-  static std::vector<std::pair<const void*, int>> done;
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  std::lock_guard<std::mutex> lock(mu);
-  for (const auto& d : done)
-    if (d.first == fn && d.second == dev) return hipSuccess;
-  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  if (e == hipSuccess) done.emplace_back(fn, dev);
-  return e;
-}
-
 // ---------------------------------------------------------------- activation quantisation
 // One block per sequence: x (or the token's embedding row, also copied to x_out) -> RMSNorm
 // with runq's sum of squares -> runq's quantisation into p.xq / p.xqs.  Dynamic LDS: the
@@ -285,8 +268,6 @@ __global__ void __launch_bounds__(W * 64) gemv_q8_exact_kernel(GemvParams p) {
 
 template <int MODE, bool NT, int W>
 static hipError_t launch_q8x_w(const GemvParams& p, hipStream_t s, size_t lds) {
-  const hipError_t attr = lds_attr((const void*)gemv_q8_exact_kernel<MODE, NT, W>);
-  if (attr != hipSuccess) return attr;
   const int rows = MODE == GM_QKV ? 2 * p.n_items : p.n_items;
   hipLaunchKernelGGL((gemv_q8_exact_kernel<MODE, NT, W>), dim3((rows + 15) / 16), dim3(W * 64), lds, s, p);
   return hipGetLastError();
@@ -462,10 +443,41 @@ static hipError_t launch_attn_q8x_hs(const AttnParams& a, int B, float* att, hip
   if (e != hipSuccess) return e;
   const int rv = 256;  // V rows per round (a multiple of 16 and of the rows per DMA instruction)
   const size_t lds = (size_t)(64 + ((a.seq_len + 3) & ~3) + 64 * (4 * ((a.seq_len + 255) >> 8) + 4) + rv * CW) * 4;
-  const hipError_t attr = lds_attr((const void*)attn_q8x_out_kernel<HS, NG>);
-  if (attr != hipSuccess) return attr;
   hipLaunchKernelGGL((attn_q8x_out_kernel<HS, NG>), dim3(B * a.n_heads, NG), dim3(64), lds, s, a, att, rv);
   return hipGetLastError();
+}
+
+// Raise every kernel's dynamic-LDS limit to 160 KiB on the current device, once per device (the
+// attribute is per device): called when an exact int8 decoder is created, so no launch — and no
+// graph capture — ever sets an attribute.
+template <int MODE>
+static hipError_t q8x_attr_mode() {
+  const void* fns[] = {(const void*)gemv_q8_exact_kernel<MODE, true, 8>, (const void*)gemv_q8_exact_kernel<MODE, true, 6>,
+                       (const void*)gemv_q8_exact_kernel<MODE, true, 4>, (const void*)gemv_q8_exact_kernel<MODE, false, 8>,
+                       (const void*)gemv_q8_exact_kernel<MODE, false, 6>, (const void*)gemv_q8_exact_kernel<MODE, false, 4>};
+  for (const void* f : fns) {
+    const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t q8_exact_prepare() {
+  static std::mutex mu;
+  static std::vector<int> done;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lock(mu);
+  for (int d : done)
+    if (d == dev) return hipSuccess;
+  if ((e = q8x_attr_mode<GM_STORE>()) != hipSuccess || (e = q8x_attr_mode<GM_RESID>()) != hipSuccess ||
+      (e = q8x_attr_mode<GM_SWIGLU>()) != hipSuccess || (e = q8x_attr_mode<GM_QKV>()) != hipSuccess)
+    return e;
+  for (const void* f : {(const void*)attn_q8x_out_kernel<128, 8>, (const void*)attn_q8x_out_kernel<64, 8>})
+    if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) != hipSuccess) return e;
+  done.push_back(dev);
+  return hipSuccess;
 }
 
 hipError_t launch_attn_q8_exact(const AttnParams& a, int B, float* att, hipStream_t s) {

@@ -18,6 +18,7 @@
 #include "../../include/hip_helper.hpp"
 #include "../../include/thallama.h"
 #include "synth.hpp"
+#include "api_lock.hpp"
 
 // ------------------------------------------------------------------ layout
 extern "C" size_t thallama_v0_payload_floats(const Config* p, int shared_weights) {
@@ -169,6 +170,7 @@ extern "C" void copy_weight_to_device(Transformer* t_h, TransformerWeights*& w_d
   const int shared = t_h->weights.wcls == t_h->weights.token_embedding_table;
   const size_t n = thallama_v0_payload_floats(p, shared);
   float* arena = nullptr;
+  tl::ApiLock lock(tl::api_mu());
   CHECK_HIP(hipMalloc(&arena, n * sizeof(float)));
   CHECK_HIP(hipMemcpy(arena, t_h->weights.token_embedding_table, n * sizeof(float), hipMemcpyHostToDevice));
   w_d = (TransformerWeights*)malloc(sizeof(TransformerWeights));
@@ -197,6 +199,7 @@ extern "C" void alloc_state_to_device(Transformer* t_h, RunState*& s_d) { alloc_
 
 extern "C" void free_weight_device(TransformerWeights* w_d) {
   if (!w_d) return;
+  tl::ApiLock lock(tl::api_mu());
   CHECK_HIP(hipFree(w_d->token_embedding_table));
   free(w_d);
 }
@@ -207,6 +210,7 @@ extern "C" void alloc_state_to_device_batch(Transformer* t_h, RunState*& s_d_bat
   const size_t dim = p->dim, V = p->vocab_size, L = p->n_layers, H = p->n_heads, S = p->seq_len;
   const size_t hid = p->hidden_dim, kvd = (size_t)p->dim * p->n_kv_heads / p->n_heads, B = batch_size;
   RunState* s = (RunState*)calloc(1, sizeof(RunState));
+  tl::ApiLock lock(tl::api_mu());
   CHECK_HIP(hipMalloc(&s->x, dim * B * 4));
   CHECK_HIP(hipMalloc(&s->xb, dim * B * 4));
   CHECK_HIP(hipMalloc(&s->xb2, dim * B * 4));
@@ -224,6 +228,7 @@ extern "C" void alloc_state_to_device_batch(Transformer* t_h, RunState*& s_d_bat
 
 extern "C" void free_state_device(RunState* s) {
   if (!s) return;
+  tl::ApiLock lock(tl::api_mu());
   float* bufs[] = {s->x, s->xb, s->xb2, s->hb, s->hb2, s->q, s->att, s->logits, s->key_cache, s->value_cache};
   for (float* b : bufs)
     if (b) CHECK_HIP(hipFree(b));
@@ -296,6 +301,7 @@ extern "C" int thallama_synth_arena(float* arena, const Config* cfg, int shared_
                                     hipStream_t stream) {
   TlSynthPlan plan;
   tl_synth_plan(&plan, cfg, shared_weights);
+  tl::ApiLock lock(tl::api_mu());  // (launches on the legacy stream when stream is null)
   for (int t = 0; t < plan.n; ++t) {
     const TlSynthTensor& e = plan.t[t];
     if (!e.count) continue;
@@ -322,19 +328,39 @@ extern "C" int thallama_device_count(void) {
 }
 extern "C" int thallama_set_device(int dev) { return (int)hipSetDevice(dev); }
 extern "C" void* thallama_malloc(size_t bytes) {
+  tl::ApiLock lock(tl::api_mu());
   void* p = nullptr;
   if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) return nullptr;
   return p;
 }
-extern "C" int thallama_free(void* p) { return (int)hipFree(p); }
+extern "C" int thallama_free(void* p) {
+  tl::ApiLock lock(tl::api_mu());
+  return (int)hipFree(p);
+}
 extern "C" int thallama_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+  tl::ApiLock lock(tl::api_mu());
   return (int)hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice);
 }
 extern "C" int thallama_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+  tl::ApiLock lock(tl::api_mu());
   return (int)hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
 }
 extern "C" int thallama_memcpy_d2d(void* dst, const void* src, size_t bytes) {
+  tl::ApiLock lock(tl::api_mu());
   return (int)hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice);
 }
-extern "C" int thallama_memset(void* dst, int value, size_t bytes) { return (int)hipMemset(dst, value, bytes); }
-extern "C" int thallama_sync(void) { return (int)hipDeviceSynchronize(); }
+extern "C" int thallama_memset(void* dst, int value, size_t bytes) {
+  tl::ApiLock lock(tl::api_mu());
+  return (int)hipMemset(dst, value, bytes);
+}
+extern "C" int thallama_sync(void) {
+  tl::ApiLock lock(tl::api_mu());
+  return (int)hipDeviceSynchronize();
+}
+
+namespace tl {
+std::recursive_mutex& api_mu() {
+  static std::recursive_mutex m;
+  return m;
+}
+}  // namespace tl

@@ -167,6 +167,7 @@ def lib():
             "thallama_decoder_prof_reset": (None, [VP]),
             "thallama_step_bytes": (C.c_double, [C.POINTER(Config), I, I, c_int_p]),
             "thallama_forward_batch_cache_size": (I, []),
+            "thallama_forward_batch_live": (I, []),
             "thallama_forward_batch_cache_clear": (None, []),
             "thallama_synth_arena": (I, [P, C.POINTER(Config), I, C.c_uint64, VP]),
             "thallama_device_count": (I, []),

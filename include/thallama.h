@@ -127,9 +127,12 @@ void thallama_decoder_prof_reset(thallama_decoder* d);
 
 /* thaDNN_s_forward_batch / thaDNN_q8_forward_batch keep one decoder per (device, stream, batch,
  * config, dtype), made for the caller's weight and state buffers; a call with other buffers
- * replaces it, and at most 8 live at once (least recently used freed).  The count, and a way to
- * free them all (e.g. before the caller frees its buffers). */
+ * replaces it, and at most 8 stay cached (least recently used dropped).  Concurrent callers are
+ * safe: a dropped decoder is freed when the last call using it returns.  The cached count, the
+ * live count (cached + dropped but still running), and a way to drop them all (e.g. before the
+ * caller frees its buffers). */
 int thallama_forward_batch_cache_size(void);
+int thallama_forward_batch_live(void);
 void thallama_forward_batch_cache_clear(void);
 
 /* Algorithmic HBM bytes of one step for kernel class kclass at the given positions
