@@ -48,8 +48,58 @@ def run(name="llama2_7b", batch=1, steps=None):
     return out
 
 
+def run_forced(config, shared, seed, tokens, probe_ids, full_steps=()):
+    """Teacher-forced decode along `tokens` (step i at position i) with the reference's GPU
+    forward_batch: (probe_vals [n][k] at probe_ids [n][k], {step: full logits})."""
+    lib = C.CDLL(os.path.join(REPO, "oracle", "_ref", "libref_gpu.so"))
+    ip = C.POINTER(C.c_int)
+    fpp = C.POINTER(C.c_float)
+    lib.refgpu_forced.restype = C.c_int
+    lib.refgpu_forced.argtypes = [ip, C.c_int, C.c_ulonglong, ip, C.c_int, C.c_int, ip, C.c_int, fpp, ip, C.c_int, fpp]
+    tok = np.ascontiguousarray(tokens, np.int32)
+    ids = np.ascontiguousarray(probe_ids, np.int32)
+    n, k = ids.shape
+    assert tok.size == n
+    V = abs(config[5])
+    vals = np.zeros((n, k), np.float32)
+    fs = np.ascontiguousarray(list(full_steps) or [-1], np.int32)
+    full = np.zeros((len(fs), V), np.float32)
+    cfg = (C.c_int * 7)(*config)
+    st = lib.refgpu_forced(cfg, int(shared), int(seed), tok.ctypes.data_as(ip), 0, n, ids.ctypes.data_as(ip), k,
+                           vals.ctypes.data_as(fpp), fs.ctypes.data_as(ip), len(full_steps), full.ctypes.data_as(fpp))
+    if st != 0:
+        raise RuntimeError(f"refgpu_forced: status {st}")
+    return vals, {int(s): full[i] for i, s in enumerate(full_steps)}
+
+
+def forced_2048(out_path):
+    """tests/golden/reference_gpu_drift_2048.json: the reference GPU path's drift from the CPU
+    fixture (reference_2048.json) along its tokens, per step (max over the step's probe logits;
+    whole logits at steps 255, 1023, 2047) — the yardstick of test_golden_2048_gpu.py."""
+    g = os.path.join(REPO, "tests", "golden")
+    with open(os.path.join(g, "reference_2048.json")) as f:
+        fx = json.load(f)
+    npz = np.load(os.path.join(g, "reference_2048_logits.npz"))
+    toks = [fx["start_token"]] + fx["tokens"][:-1]
+    ids, vals = npz["probe_ids"], npz["probe_vals"].astype(np.float64)
+    got, full = run_forced(fx["config"], fx["shared"], fx["seed"], toks, ids, (255, 1023, 2047))
+    d = np.abs(got.astype(np.float64) - vals).max(axis=1)
+    for p in (255, 1023, 2047):
+        d[p] = max(d[p], np.abs(full[p].astype(np.float64) - npz[f"step{p}"].astype(np.float64)).max())
+    rec = {"generator": "tools/ref_gpu.py --forced-2048 (oracle/_ref/libref_gpu.so: the reference's "
+                        "thaDNN_s_forward_batch, src/thaDNN.cpp:13-82, built for gfx950)",
+           "max_drift": float(d.max()), "argmax": int(d.argmax()), "drift": [float(x) for x in d]}
+    with open(out_path, "w") as f:
+        json.dump(rec, f)
+    return rec
+
+
 if __name__ == "__main__":
     a = sys.argv[1:]
+    if "--forced-2048" in a:
+        r = forced_2048(a[a.index("--forced-2048") + 1])
+        print(json.dumps({"max_drift": r["max_drift"], "argmax": r["argmax"]}), flush=True)
+        sys.exit(0)
     name = a[0] if a and not a[0].startswith("-") else "llama2_7b"
     batch = int(a[a.index("--batch") + 1]) if "--batch" in a else 1
     steps = int(a[a.index("--steps") + 1]) if "--steps" in a else None
