@@ -10,19 +10,23 @@ Workloads (one "step" = one pass of the hot path over one batch of synthetic inp
   K timed decodes.  The line also carries the long-context tail (positions 1792..2047 of a
   2048-token decode, the length the reference's test mode runs to), the 1-GPU point of the
   request workload below, the dominant kernel's roofline and the CPU baseline.
-* ``requests`` (default at N > 1; BASELINE.json configs[4]): the reference's test mode
-  (src/llama.cpp:891-1083) over its assets/in/gen_in_64.txt prompts — 8 prompts per GPU
-  (--prompts-per-gpu; all 64 at N = 8), 8 slots per GPU, greedy, prompt prefilled, each request
-  decoded to position 255 or EOS/BOS.  A step is one pass over the job; value = the reference's
-  token count (sum of pos - 1 over requests, src/llama.cpp:1062) / time, max over ranks.  The
-  output file rank 0 gathers is compared with a committed one-process fixture.
+* ``cli`` (default at N > 1; BASELINE.json configs[4]): the drop-in's own multi-GPU path — the
+  CLI build/apps/llama in test mode (src/llama.cpp:891-1083: one host thread per GPU, weights
+  uploaded once and RCCL-broadcast over xGMI) over the reference's assets/in/gen_in_64.txt
+  prompts: 8 per GPU (--prompts-per-gpu; all 64 at N = 8), 8 slots per GPU, greedy (-g 1),
+  prompts prefilled, each request to position 255 or EOS/BOS.  A step is one pass over the job;
+  value = the reference's token count (sum of pos - 1 over requests, src/llama.cpp:1062) / the
+  CLI's serve time.  The output file is compared with a committed one-process fixture.
+* ``requests``: the same job through a torch.distributed process-per-GPU harness
+  (hip_llama_cpp_amd/dist.py over the HIP decoder's native callbacks) — a cross-check of the CLI.
 
-Multi-GPU: one process per GPU.  ``--gpus N`` with no WORLD_SIZE in the environment starts the N
-ranks itself (torch.distributed.run as a child process, before anything touches a GPU) and exits
-with their status; under an outer torch.distributed.run it is one rank.  Rank 0 synthesises the
-weights once and RCCL-broadcasts them over xGMI; no collective on the data path (weak scaling).
+Multi-GPU: ``--gpus N`` with no WORLD_SIZE in the environment starts the N ranks itself
+(torch.distributed.run as a child process, before anything touches a GPU) and exits with their
+status; under an outer torch.distributed.run it is one rank.  ``cli``: rank 0 starts the CLI over
+GPUs 0..N-1, the other ranks wait.  ``requests``/``decode``: rank 0 synthesises the weights once
+and RCCL-broadcasts them; no collective on the data path (weak scaling).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload decode|requests]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload decode|cli|requests]
                     [--model 7b|110m] [--dtype f32|int8] [--batch B]
 """
 import argparse
@@ -59,8 +63,10 @@ def parse_args(argv):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5, help="timed steps (decodes / request passes)")
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["decode", "requests"], default=None,
-                    help="default: decode at N = 1, requests at N > 1")
+    ap.add_argument("--workload", choices=["decode", "requests", "cli"], default=None,
+                    help="default: decode at N = 1, cli at N > 1 (requests: the torch.distributed cross-check)")
+    ap.add_argument("--cli-replicas", type=int, default=0,
+                    help="cli: THALLAMA_REPLICAS (more workers than GPUs: a one-GPU rehearsal of the N-GPU split)")
     ap.add_argument("--decode-len", type=int, default=256, help="positions per sequence (configs[2]: 256)")
     ap.add_argument("--model", default="7b", choices=sorted(MODELS))
     ap.add_argument("--dtype", default="f32", choices=["f32", "int8"])
@@ -177,6 +183,112 @@ def plumbing(args, world, rank):
         dist.destroy_process_group()
 
 
+# ---------------------------------------------------------------- --workload cli (configs[4])
+def cli_run(args, world, rank):
+    """BASELINE.json configs[4] through the drop-in's OWN multi-GPU path: the CLI
+    (build/apps/llama, app/run.cpp — the reference's test_data_parallelism, src/llama.cpp:891-1083:
+    one host thread per GPU, one slot batch per thread, one weight upload then an RCCL broadcast
+    over xGMI) serving the first prompts_per_gpu x N prompts of gen_in_64.txt greedily (-g 1) with
+    B slots per GPU, each request to position decode_len - 1 or EOS/BOS.  The weights are the
+    synthetic model made on GPU 0 ("synth:" spec, no 27 GB file).  Rank 0 starts the CLI as a child
+    process over GPUs 0..N-1 before anything here touches a GPU; other ranks only wait (gloo).
+    The CLI serves the file warmup + steps times on the same resident weights (THALLAMA_PASSES);
+    value = tokens of the timed passes / their serve time (the CLI's own clock, weights already
+    in HBM); the output file is compared byte for byte with the committed one-process fixture."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group(backend="gloo")
+    res = None
+    if rank == 0:
+        cfg_t, shared, mname = MODELS[args.model]
+        q8 = args.dtype == "int8"
+        T, B = args.decode_len, args.batch or 8
+        n = args.prompts_per_gpu * world
+        if n > 64:
+            raise SystemExit(f"{n} prompts > the 64 of gen_in_64.txt")
+        exe = os.path.join(REPO, "build", "apps", "llama")
+        if not os.path.exists(exe):
+            raise SystemExit(f"bench.py: {exe} not built (make -C hip_llama.cpp_amd)")
+        dims = list(cfg_t)
+        dims[5] = dims[5] if shared else -dims[5]
+        spec = "synth:" + ",".join(str(v) for v in dims) + f":{SEED}" + (f":q8:{args.group_size}" if q8 else "")
+        wd = tempfile.mkdtemp(prefix=".bench_cli_", dir=REPO)
+        req = write_requests(read_prompts(PROMPTS, n), wd)
+        out = os.path.join(wd, "out.txt")
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if "HIP_VISIBLE_DEVICES" not in env and "ROCR_VISIBLE_DEVICES" not in env:
+            env["HIP_VISIBLE_DEVICES"] = ",".join(str(i) for i in range(world))
+        if args.cli_replicas:
+            env["THALLAMA_REPLICAS"] = str(args.cli_replicas)
+        env["THALLAMA_PASSES"] = str(args.warmup + args.steps)
+        env["THALLAMA_TEST_STEPS"] = str(T)
+        cmd = [exe, spec, "-m", "test", "-f", req, "-o", out, "-b", str(B), "-g", "1", "-z", TOKENIZER]
+        log("bench.py: " + " ".join(cmd))
+        t0 = time.perf_counter()
+        p = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True)
+        wall = time.perf_counter() - t0
+        if p.returncode != 0:
+            log(p.stdout[-4000:], p.stderr[-4000:])
+            raise SystemExit(f"bench.py: the CLI failed ({p.returncode})")
+        passes = [(int(ln.split()[3]), float(ln.split()[5])) for ln in p.stdout.splitlines()
+                  if ln.startswith("pass ")]
+        if not passes:  # one pass: the reference's own summary lines
+            tot = [ln for ln in p.stdout.splitlines() if ln.startswith("Total achieved token:")]
+            el = [ln for ln in p.stdout.splitlines() if ln.startswith("elapsed time(s):")]
+            passes = [(int(tot[-1].split()[-1]), float(el[-1].split()[2].rstrip(",")))]
+        timed_p = passes[args.warmup:] or passes
+        tokens = sum(t for t, _ in timed_p)
+        secs = sum(x for _, x in timed_p)
+        load = next((float(ln.split()[-1]) for ln in p.stdout.splitlines() if ln.startswith("Load model time")), None)
+        with open(out, "rb") as f:
+            got = f.read()
+        fx_path = os.path.join(GOLDEN, f"bench_requests_{mname}_{args.dtype}_greedy.json")
+        match = None
+        if os.path.exists(fx_path):
+            with open(fx_path) as f:
+                fx = json.load(f)
+            if fx.get("decode_len") == T and fx.get("seed") == SEED and len(fx["outputs"]) >= n:
+                want = f"{n}\n".encode() + b"".join(o.encode("utf-8", "surrogateescape") + b"\n"
+                                                      for o in fx["outputs"][:n])
+                match = got == want
+        # algorithmic bytes: every decode step of a GPU reads the weights once for its B slots plus
+        # each slot's K/V rows; requests here run from their prompt to T - 1
+        wbytes = 4.0 * (cfg_t[2] * (2 * cfg_t[0] ** 2 + 2 * cfg_t[0] * cfg_t[0] * cfg_t[4] // cfg_t[3]
+                                    + 3 * cfg_t[0] * cfg_t[1]) + cfg_t[5] * cfg_t[0])
+        res = {"metric": "decode tokens/sec (greedy, whole model) + achieved HBM GB/s fraction",
+               "value": round(tokens / secs, 3), "unit": "tok/s", "n_gpus": world, "steps": len(timed_p),
+               "warmup": args.warmup, "ms_per_step": round(1e3 * secs / len(timed_p), 3),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+               "data": "synthetic weights (random init, seed 20240224, made on GPU 0); prompts: the reference's "
+                       "gen_in_64.txt",
+               "config": {"workload": f"{mname} {args.dtype} drop-in CLI test mode (build/apps/llama -m test -g 1 "
+                                      f"-b {B}; src/llama.cpp:891-1083), {n} prompts of gen_in_64.txt "
+                                      f"({args.prompts_per_gpu} per GPU, one host thread + RCCL-broadcast replica per "
+                                      f"GPU), each request to position {T - 1} or EOS/BOS",
+                          "model": mname, "global_batch": n, "slots_per_gpu": B, "seq_len": cfg_t[6], "decode_len": T,
+                          "parallelism": f"prompt-dp{world} (threads + RCCL broadcast)"},
+               "cli": {"cmd": " ".join(os.path.relpath(c, REPO) if c.startswith(REPO) else c for c in cmd),
+                       "passes": [{"tokens": t, "seconds": x} for t, x in passes],
+                       "load_s": load, "wall_s": round(wall, 2), "replicas": args.cli_replicas or world,
+                       "output_matches_fixture": match,
+                       "fixture": os.path.relpath(fx_path, REPO) if os.path.exists(fx_path) else None,
+                       "output_sha": hashlib.sha256(got).hexdigest()[:16]},
+               "roofline": None,
+               "roofline_note": "the CLI runs in a child process: per-kernel HIP events are in the N = 1 decode line; "
+                                f"weights {wbytes / 1e9:.2f} GB read once per step for {B} slots",
+               "cpu_baseline": None}
+        for f_ in (req, out):
+            os.remove(f_)
+        os.rmdir(wd)
+    if world > 1:
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 # ---------------------------------------------------------------- GPU
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
@@ -195,7 +307,9 @@ def main(argv=None):
         return plumbing(args, world, rank)
     if args.device_map:
         local = [int(v) for v in args.device_map.split(",")][local]
-    workload = args.workload or ("decode" if world == 1 else "requests")
+    workload = args.workload or ("decode" if world == 1 else "cli")
+    if workload == "cli":
+        return cli_run(args, world, rank)
 
     import torch
     import torch.distributed as dist

@@ -72,17 +72,63 @@ static void error_usage() {
 }
 
 // The model file: a llama2.c v0 fp32 checkpoint (src/utils.cpp:150-170) or a runq v2 "ak42"
-// int8 checkpoint (runq.c:219-251), told apart by the v2 magic.
+// int8 checkpoint (runq.c:219-251), told apart by the v2 magic.  Not in the reference: a
+// synthetic model, "synth:dim,hidden,layers,heads,kv_heads,vocab,seq_len:seed[:q8:gs]" (vocab < 0 =
+// unshared classifier, as in the v0 header) — the deterministic generator of include/
+// thallama_synth.h run on GPU 0 (int8: quantised there with export.py semantics) instead of a
+// file read, so a 27 GB llama2-7B needs no model file (bench.py's CLI workload).
 struct ModelFile {
   bool q8 = false;
+  bool synth = false;
+  unsigned long long seed = 0;
+  int shared = 0, gs = 0;
   Transformer t{};     // v0: mmapped fp32 model (build_transformer)
   Q8Checkpoint ck{};   // v2: mmapped int8 payload
   Config cfg{};
-  const void* payload = nullptr;  // host image of the device arena
+  const void* payload = nullptr;  // host image of the device arena (nullptr: synthesised on GPU 0)
   size_t bytes = 0;
 };
 
+static void print_config(const Config& c) {
+  printf("dim: %d\nhidden_dim: %d\nn_layers: %d\nn_heads: %d\nn_kv_heads: %d\nvocab_size: %d\nseq_len: %d\n", c.dim,
+         c.hidden_dim, c.n_layers, c.n_heads, c.n_kv_heads, c.vocab_size, c.seq_len);
+}
+
+static bool open_synth(ModelFile& m, const char* spec) {
+  int v[7];
+  unsigned long long seed = 0;
+  char q8tag[8] = {0};
+  int gs = 64;
+  const int n = sscanf(spec, "synth:%d,%d,%d,%d,%d,%d,%d:%llu:%2s:%d", &v[0], &v[1], &v[2], &v[3], &v[4], &v[5], &v[6],
+                       &seed, q8tag, &gs);
+  if (n < 8 || v[0] <= 0 || v[2] <= 0 || v[3] <= 0 || v[4] <= 0 || v[5] == 0 || v[6] <= 0) return false;
+  m.synth = true;
+  m.seed = seed;
+  m.shared = v[5] > 0;
+  m.cfg = Config{v[0], v[1], v[2], v[3], v[4], v[5] < 0 ? -v[5] : v[5], v[6]};
+  m.t.config = m.cfg;
+  if (n >= 9 && strcmp(q8tag, "q8") == 0) {
+    m.q8 = true;
+    m.gs = gs;
+    m.bytes = thallama_q8_payload_bytes(&m.cfg, m.shared, gs);
+  } else {
+    m.bytes = thallama_v0_payload_floats(&m.cfg, m.shared) * sizeof(float);
+  }
+  printf("---------Model Information----------\n");
+  printf("synthetic %s model, seed %llu%s\n", m.q8 ? "int8" : "fp32", seed, m.shared ? ", shared classifier" : "");
+  print_config(m.cfg);
+  printf("------------------------------------\n");
+  return true;
+}
+
 static void open_model(ModelFile& m, char* path) {
+  if (strncmp(path, "synth:", 6) == 0) {
+    if (!open_synth(m, path)) {
+      fprintf(stderr, "bad synthetic model spec %s\n", path);
+      exit(EXIT_FAILURE);
+    }
+    return;
+  }
   FILE* f = fopen(path, "rb");
   if (!f) {
     fprintf(stderr, "Couldn't open file %s\n", path);
@@ -99,27 +145,56 @@ static void open_model(ModelFile& m, char* path) {
     }
     m.q8 = true;
     m.cfg = m.ck.config;
+    m.shared = m.ck.shared_classifier;
+    m.gs = m.ck.group_size;
     m.payload = m.ck.payload;
-    m.bytes = thallama_q8_payload_bytes(&m.cfg, m.ck.shared_classifier, m.ck.group_size);
+    m.bytes = thallama_q8_payload_bytes(&m.cfg, m.shared, m.gs);
     m.t.config = m.cfg;
     printf("---------Model Information----------\n");
-    printf("int8 (runq v2) group_size: %d\n", m.ck.group_size);
-    printf("dim: %d\nhidden_dim: %d\nn_layers: %d\nn_heads: %d\nn_kv_heads: %d\nvocab_size: %d\nseq_len: %d\n",
-           m.cfg.dim, m.cfg.hidden_dim, m.cfg.n_layers, m.cfg.n_heads, m.cfg.n_kv_heads, m.cfg.vocab_size,
-           m.cfg.seq_len);
+    printf("int8 (runq v2) group_size: %d\n", m.gs);
+    print_config(m.cfg);
     printf("------------------------------------\n");
   } else {
     build_transformer(&m.t, path);
     m.cfg = m.t.config;
-    const int shared = m.t.weights.wcls == m.t.weights.token_embedding_table;
+    m.shared = m.t.weights.wcls == m.t.weights.token_embedding_table;
     m.payload = m.t.weights.token_embedding_table;
-    m.bytes = thallama_v0_payload_floats(&m.cfg, shared) * sizeof(float);
+    m.bytes = thallama_v0_payload_floats(&m.cfg, m.shared) * sizeof(float);
   }
 }
 
 static void close_model(ModelFile& m) {
+  if (m.synth) return;
   if (m.q8) thallama_q8_close_checkpoint(&m.ck);
   else free_transformer(&m.t);
+}
+
+// A synthetic model's weight image, made on the current device in `arena` (m.bytes).
+static void synth_on_device(const ModelFile& m, void* arena) {
+  Config hdr = m.cfg;  // (positive vocab; the classifier sharing is the flag, as in bench.py)
+  if (!m.q8) {
+    if (thallama_synth_arena((float*)arena, &hdr, m.shared, m.seed, nullptr) != 0) {
+      fprintf(stderr, "synthetic weights: %s\n", thallama_last_error());
+      exit(EXIT_FAILURE);
+    }
+  } else {
+    const size_t nf = thallama_v0_payload_floats(&hdr, m.shared);
+    float* fp = nullptr;
+    HIP_OK(hipMalloc(&fp, nf * sizeof(float)));
+    TransformerWeights w{};
+    if (thallama_synth_arena(fp, &hdr, m.shared, m.seed, nullptr) != 0) {
+      fprintf(stderr, "synthetic weights: %s\n", thallama_last_error());
+      exit(EXIT_FAILURE);
+    }
+    thallama_map_weights(&w, &hdr, fp, m.shared);
+    if (thallama_q8_quantize_model(arena, &w, &m.cfg, m.shared, m.gs, nullptr) != 0) {
+      fprintf(stderr, "int8 quantisation: %s\n", thallama_last_error());
+      exit(EXIT_FAILURE);
+    }
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipFree(fp));
+  }
+  HIP_OK(hipDeviceSynchronize());
 }
 
 // One GPU's replica: the weight arena, run state for `batch` sequences, the decoder.
@@ -145,7 +220,8 @@ static std::vector<Replica> replicate(ModelFile& m, int n_dev, int n_rep, int ba
     HIP_OK(hipMalloc(&reps[d].arena, m.bytes));
   }
   HIP_OK(hipSetDevice(0));
-  HIP_OK(hipMemcpy(reps[0].arena, m.payload, m.bytes, hipMemcpyHostToDevice));
+  if (m.payload) HIP_OK(hipMemcpy(reps[0].arena, m.payload, m.bytes, hipMemcpyHostToDevice));
+  else synth_on_device(m, reps[0].arena);
   if (n_dev > 1) {
     std::vector<ncclComm_t> comms((size_t)n_dev);
     std::vector<int> devs((size_t)n_dev);
@@ -183,7 +259,7 @@ static std::vector<Replica> replicate(ModelFile& m, int n_dev, int n_rep, int ba
     int rc;
     if (m.q8) {
       HIP_OK(hipMalloc(&r.emb, sizeof(float) * (size_t)m.cfg.vocab_size * m.cfg.dim));
-      if (thallama_q8_map(&r.w8, &m.cfg, r.arena, m.ck.shared_classifier, m.ck.group_size, r.emb) != 0 ||
+      if (thallama_q8_map(&r.w8, &m.cfg, r.arena, m.shared, m.gs, r.emb) != 0 ||
           thallama_q8_dequant_embedding(&r.w8, &m.cfg, nullptr) != 0) {
         fprintf(stderr, "int8 weights on device %d: %s\n", d, thallama_last_error());
         exit(EXIT_FAILURE);
@@ -191,8 +267,7 @@ static std::vector<Replica> replicate(ModelFile& m, int n_dev, int n_rep, int ba
       HIP_OK(hipDeviceSynchronize());
       rc = thallama_decoder_create_q8(&r.dec, &m.cfg, &r.w8, r.s, batch, nullptr);
     } else {
-      const int shared = m.t.weights.wcls == m.t.weights.token_embedding_table;
-      thallama_map_weights(&r.w, &m.cfg, (float*)r.arena, shared);
+      thallama_map_weights(&r.w, &m.cfg, (float*)r.arena, m.shared);
       rc = thallama_decoder_create(&r.dec, &m.cfg, &r.w, r.s, batch, nullptr);
     }
     if (rc != 0) {
@@ -360,6 +435,11 @@ int main(int argc, char* argv[]) {
     // chat() is commented out in the reference's main (src/llama.cpp:1590)
   } else if (strcmp(mode, "test") == 0) {
     steps = model.cfg.seq_len;
+    // THALLAMA_TEST_STEPS=T (not in the reference, which always decodes to seq_len in test mode):
+    // each request to position T - 1 at most (bench.py's 256-position request workload)
+    if (getenv("THALLAMA_TEST_STEPS") && atoi(getenv("THALLAMA_TEST_STEPS")) > 1 &&
+        atoi(getenv("THALLAMA_TEST_STEPS")) < steps)
+      steps = atoi(getenv("THALLAMA_TEST_STEPS"));
     if (!input_filename || !output_filename) error_usage();
     const int max_token_len = thallama_tokenizer_max_token_length(tok);
     printf("max_token_len: %d, max_seq_len: %d\n", max_token_len, steps);
@@ -377,27 +457,42 @@ int main(int argc, char* argv[]) {
     // the GPUs there are (a rehearsal of an N-GPU run: the worker split, the per-replica decoders)
     const char* rep_env = getenv("THALLAMA_REPLICAS");
     const int n_rep = rep_env && atoi(rep_env) > 0 ? atoi(rep_env) : n_dev;
+    // THALLAMA_PASSES=P (not in the reference; bench.py): serve the request file P times on the
+    // same resident weights, one "pass i: ..." line each; the output file is the last pass's
+    const char* pass_env = getenv("THALLAMA_PASSES");
+    const int passes = pass_env && atoi(pass_env) > 0 ? atoi(pass_env) : 1;
     fprintf(stderr, "\n DATA PARALLELISM \n");
     fprintf(stderr, "\n Num Devices %d\n", n_rep);
     fprintf(stderr, "\n Batch Size %d\n", batch);
     const long load_start = time_in_ms();
     std::vector<Replica> reps = replicate(model, n_dev, n_rep, batch);
-    fprintf(stdout, "\nLoad model time (1 upload + RCCL broadcast to %d GPUs): %f\n", n_dev,
-            (double)(time_in_ms() - load_start) / 1000);
+    fprintf(stdout, "\nLoad model time (1 %s + RCCL broadcast to %d GPUs): %f\n",
+            model.synth ? "on-device synthesis" : "upload", n_dev, (double)(time_in_ms() - load_start) / 1000);
 
-    const long start = time_in_ms();
-    long long num_gen_tokens = 0;
-    const int st = thallama_serve_requests_greedy(req, tokenizer_path, V, n_rep, batch, replica_step,
-                                                  getenv("THALLAMA_HOST_ARGMAX") ? nullptr : replica_argmax,
-                                                  replica_prefill, &reps, &num_gen_tokens);
-    const long end = time_in_ms();
-    if (st != 0) {
-      fprintf(stderr, "test mode failed (%d)\n", st);
-      exit(EXIT_FAILURE);
+    for (int pass = 0; pass < passes; ++pass) {
+      if (pass > 0) {  // a fresh copy of the requests (the scheduler fills in their outputs)
+        thallama_requests_free(req);
+        req = thallama_requests_read(input_filename, max_token_len, steps);
+        if (!req) exit(EXIT_FAILURE);
+        if (greedy_test) thallama_requests_set_sampling(req, 0.0f, 0.9f);
+      }
+      const long start = time_in_ms();
+      long long num_gen_tokens = 0;
+      const int st = thallama_serve_requests_greedy(req, tokenizer_path, V, n_rep, batch, replica_step,
+                                                    getenv("THALLAMA_HOST_ARGMAX") ? nullptr : replica_argmax,
+                                                    replica_prefill, &reps, &num_gen_tokens);
+      const long end = time_in_ms();
+      if (st != 0) {
+        fprintf(stderr, "test mode failed (%d)\n", st);
+        exit(EXIT_FAILURE);
+      }
+      if (passes > 1)
+        fprintf(stdout, "pass %d: tokens %lld seconds %f\n", pass, num_gen_tokens, (double)(end - start) / 1000);
+      if (pass + 1 < passes) continue;
+      fprintf(stdout, "Total achieved token: %lld\n", num_gen_tokens);
+      fprintf(stdout, "elapsed time(s): %f, achieved throughput(tok/s): %f\n", (double)(end - start) / 1000,
+              num_gen_tokens / (double)(end - start) * 1000);
     }
-    fprintf(stdout, "Total achieved token: %lld\n", num_gen_tokens);
-    fprintf(stdout, "elapsed time(s): %f, achieved throughput(tok/s): %f\n", (double)(end - start) / 1000,
-            num_gen_tokens / (double)(end - start) * 1000);
     if (thallama_requests_write(req, output_filename) != 0) {
       fprintf(stderr, "cannot write output file: %s\n", input_filename);
       exit(EXIT_FAILURE);
