@@ -122,6 +122,7 @@ static constexpr int kAttnChunk = 32;  // keys per attention wave unit
 // batched prefill (thallama_decoder_prefill): tokens per chunk and attention splits per token
 static constexpr int kPrefillChunk = 128;
 static constexpr int kPrefillMaxSplits = 16;
+static constexpr int kPrefillQ8Chunk = 8;  // int8: the exact batched kernels take up to 8 sequences
 
 struct thallama_decoder {
   Config cfg;
@@ -189,6 +190,7 @@ struct thallama_decoder {
   unsigned* pf_cnt = nullptr;
   int *pf_tok = nullptr, *pf_pos = nullptr;
   int* pf_tok_h = nullptr;      // pinned staging of a chunk's prompt tokens
+  float* pf_att = nullptr;      // int8 prefill: exact attention scores [8][H][S]
   std::string pwhy;             // why not
   // profiling
   std::vector<hipEvent_t> ev_pool;
@@ -463,7 +465,7 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   (void)hipFree(d->pbmax);
   (void)hipFree(d->pgran);
   (void)hipFree(d->ptrace);
-  for (void* b : {(void*)d->pf_x, (void*)d->pf_xn, (void*)d->pf_q, (void*)d->pf_xb, (void*)d->pf_hb,
+  for (void* b : {(void*)d->pf_att, (void*)d->pf_x, (void*)d->pf_xn, (void*)d->pf_q, (void*)d->pf_xb, (void*)d->pf_hb,
                   (void*)d->pf_part, (void*)d->pf_cnt, (void*)d->pf_tok, (void*)d->pf_pos})
     (void)hipFree(b);
   if (d->own_stream) (void)hipStreamDestroy(d->stream);
@@ -572,12 +574,29 @@ static void norm_from_ssq(const thallama_decoder* d, tl::GemvParams& p) {
   p.ssq_nt = (d->dim + 15) / 16;
 }
 
-static int enqueue_step(thallama_decoder* d) {
-  const int dim = d->dim, hid = d->hidden, kvd = d->kv_dim, S = d->S;
-  const long long kv_b_stride = (long long)d->L * S * kvd;
-  const TransformerWeights& w = d->w;
+// Where a multi-launch step reads and writes: the decoder's RunState for its B sequences, or
+// (prefill) a chunk of one sequence's prompt tokens as nb "sequences" at their own positions over
+// that sequence's cache (kv_b_stride 0), with no classifier.
+struct StepIO {
+  float *x, *xb, *q, *hb, *logits;  // logits == nullptr: layers only
+  float *kc, *vc;
+  long long kv_b_stride;
+  int *tok, *pos;
+  int nb;
+  float* att;  // int8 exact attention scores [nb][H][S]
+};
+
+static StepIO step_io(thallama_decoder* d) {
   const RunState& s = d->s;
-  d->ssq_carry = ssq_carry_ok(d);
+  return StepIO{s.x, s.xb, s.q, s.hb, s.logits, s.key_cache, s.value_cache, (long long)d->L * d->S * d->kv_dim,
+                d->tok_d, d->pos_d, d->B, d->q8att_d};
+}
+
+static int enqueue_step_io(thallama_decoder* d, const StepIO& io) {
+  const int dim = d->dim, hid = d->hidden, kvd = d->kv_dim, S = d->S;
+  const long long kv_b_stride = io.kv_b_stride;
+  const TransformerWeights& w = d->w;
+  d->ssq_carry = ssq_carry_ok(d) && io.nb == d->B;
   for (int l = 0; l < d->L; ++l) {
     const long long ll = l;
     // 1. QKV (+ embedding at layer 0)
@@ -588,22 +607,22 @@ static int enqueue_step(thallama_decoder* d) {
       p.W2 = w.wv + ll * dim * kvd;
       p.K = dim;
       p.n_items = (dim + 2 * kvd) / 2;
-      p.nb = d->B;
-      p.x = s.x;
+      p.nb = io.nb;
+      p.x = io.x;
       p.x_stride = dim;
       p.rms_w = w.rms_att_weight + ll * dim;
       p.xn = d->xn_d;
       if (l > 0) norm_from_ssq(d, p);
       if (l == 0) {
-        p.tok = d->tok_d;
+        p.tok = io.tok;
         p.emb = w.token_embedding_table;
-        p.x_out = s.x;
+        p.x_out = io.x;
       }
-      p.y = s.q;
+      p.y = io.q;
       p.y_stride = dim;
-      p.pos = d->pos_d;
-      p.kc = s.key_cache;
-      p.vc = s.value_cache;
+      p.pos = io.pos;
+      p.kc = io.kc;
+      p.vc = io.vc;
       p.kv_b_stride = kv_b_stride;
       p.kv_l_off = ll * S * kvd;
       p.dim = dim;
@@ -617,13 +636,13 @@ static int enqueue_step(thallama_decoder* d) {
     // 2. attention
     {
       tl::AttnParams a = {};
-      a.q = s.q;
-      a.kc = s.key_cache;
-      a.vc = s.value_cache;
+      a.q = io.q;
+      a.kc = io.kc;
+      a.vc = io.vc;
       a.kv_b_stride = kv_b_stride;
       a.kv_l_off = ll * S * kvd;
-      a.pos = d->pos_d;
-      a.out = s.xb;
+      a.pos = io.pos;
+      a.out = io.xb;
       a.part = d->part_d;
       a.dim = dim;
       a.kv_dim = kvd;
@@ -638,16 +657,16 @@ static int enqueue_step(thallama_decoder* d) {
       int ev = prof_begin(d);
       if (d->q8x) {
         // int8 in runq's order: scores, softmax and the column chains of q8_exact.hip
-        TL_TRY(tl::launch_attn_q8_exact(a, d->B, d->q8att_d, d->stream));
+        TL_TRY(tl::launch_attn_q8_exact(a, io.nb, io.att, d->stream));
       } else if (d->hs == 64 || d->hs == 128 || d->hs == 256) {
         // wave-level units, in-kernel combine (attention.hpp: attn_wave_kernel)
         tl::AttnWaveParams wp = {};
         wp.a = a;
         wp.cnt = d->cnt_d;
-        wp.B = d->B;
+        wp.B = io.nb;
         const int max_chunks = (S + kAttnChunk - 1) / kAttnChunk;
         wp.NS = d->nsplit < max_chunks ? d->nsplit : max_chunks;
-        const int units = d->B * d->H * wp.NS;
+        const int units = io.nb * d->H * wp.NS;
         if (q8_attn_quant(d)) {
           wp.xq8 = d->xq_d;
           wp.xq8s = d->xqs_d;
@@ -661,7 +680,7 @@ static int enqueue_step(thallama_decoder* d) {
         TL_TRY(hipGetLastError());
       } else {
         // generic head sizes: block kernel + separate combine launch
-        dim3 grid(d->H, d->B, d->nsplit);
+        dim3 grid(d->H, io.nb, d->nsplit);
       switch (lpk) {
         case 2: hipLaunchKernelGGL(tl::attn_decode_kernel<2>, grid, dim3(256), lds, d->stream, a); break;
         case 4: hipLaunchKernelGGL(tl::attn_decode_kernel<4>, grid, dim3(256), lds, d->stream, a); break;
@@ -675,7 +694,7 @@ static int enqueue_step(thallama_decoder* d) {
       }
       TL_TRY(hipGetLastError());
       if (d->nsplit > 1) {
-        hipLaunchKernelGGL(tl::attn_combine_kernel<0>, dim3(d->H, d->B), dim3(128), 0, d->stream, a);
+        hipLaunchKernelGGL(tl::attn_combine_kernel<0>, dim3(d->H, io.nb), dim3(128), 0, d->stream, a);
         TL_TRY(hipGetLastError());
       }
       }
@@ -687,10 +706,10 @@ static int enqueue_step(thallama_decoder* d) {
       p.W0 = w.wo + ll * dim * dim;
       p.K = dim;
       p.n_items = dim;
-      p.nb = d->B;
-      p.x = s.xb;
+      p.nb = io.nb;
+      p.x = io.xb;
       p.x_stride = dim;
-      p.y = s.x;
+      p.y = io.x;
       p.y_stride = dim;
       p.xq_ready = q8_attn_quant(d);
       ssq_to_next_norm(d, p);
@@ -705,13 +724,13 @@ static int enqueue_step(thallama_decoder* d) {
       p.W1 = w.w3 + ll * dim * hid;
       p.K = dim;
       p.n_items = hid;
-      p.nb = d->B;
-      p.x = s.x;
+      p.nb = io.nb;
+      p.x = io.x;
       p.x_stride = dim;
       p.rms_w = w.rms_ffn_weight + ll * dim;
       p.xn = d->xn_d;
       norm_from_ssq(d, p);
-      p.y = s.hb;
+      p.y = io.hb;
       p.y_stride = hid;
       if (d->hq_d) {
         p.yq = d->hq_d;
@@ -728,10 +747,10 @@ static int enqueue_step(thallama_decoder* d) {
       p.W0 = w.w2 + ll * dim * hid;
       p.K = hid;
       p.n_items = dim;
-      p.nb = d->B;
-      p.x = s.hb;
+      p.nb = io.nb;
+      p.x = io.hb;
       p.x_stride = hid;
-      p.y = s.x;
+      p.y = io.x;
       p.y_stride = dim;
       if (d->hq_d) {
         p.xq = d->hq_d;
@@ -745,23 +764,23 @@ static int enqueue_step(thallama_decoder* d) {
     }
   }
   // final RMSNorm + classifier
-  {
+  if (io.logits) {
     tl::GemvParams p = {};
     p.W0 = w.wcls;
     p.K = dim;
     p.n_items = d->V;
-    p.nb = d->B;
-    p.x = s.x;
+    p.nb = io.nb;
+    p.x = io.x;
     p.x_stride = dim;
     p.rms_w = w.rms_final_weight;
     p.xn = d->xn_d;
     if (d->L > 0) norm_from_ssq(d, p);
     if (d->L == 0) {
-      p.tok = d->tok_d;
+      p.tok = io.tok;
       p.emb = w.token_embedding_table;
-      p.x_out = s.x;
+      p.x_out = io.x;
     }
-    p.y = s.logits;
+    p.y = io.logits;
     p.y_stride = d->V;
     int ev = prof_begin(d);
     TL_TRY(gemv(d, tl::GM_STORE, p, d->q8 ? d->w8.wcls : nullptr, nullptr, nullptr));
@@ -769,6 +788,8 @@ static int enqueue_step(thallama_decoder* d) {
   }
   return 0;
 }
+
+static int enqueue_step(thallama_decoder* d) { return enqueue_step_io(d, step_io(d)); }
 
 static bool use_persist(const thallama_decoder* d) { return d->persist && d->pok; }
 
@@ -1340,6 +1361,7 @@ extern "C" int thallama_decoder_create_q8(thallama_decoder** out, const Config* 
   if (d->q8x) {
     TL_TRY(tl::q8_exact_prepare());  // the kernels' dynamic-LDS limit, once per device
     TL_TRY(hipMalloc(&d->q8att_d, sizeof(float) * (size_t)batch * d->H * d->S));
+    if (d->pf_x) TL_TRY(hipMalloc(&d->pf_att, sizeof(float) * (size_t)kPrefillQ8Chunk * d->H * d->S));
     if (batch < 2) {  // (batch 1 multi-launch: the quantised activations' scratch too)
       const size_t kmax = (size_t)(d->dim > d->hidden ? d->dim : d->hidden);
       TL_TRY(hipMalloc(&d->xq_d, 8 * kmax));
@@ -1449,14 +1471,44 @@ static hipError_t prefill_proj(thallama_decoder* d, int mode, const tl::PGemmArg
   return gemv(d, mode, p, nullptr, nullptr, nullptr);
 }
 
+// int8 weights (runq group size 64, the exact multi-launch kernels of q8_exact.hip): chunks of up
+// to 8 prompt tokens go through the batched exact step as 8 "sequences" at their own positions over
+// slot b's cache — the QKV launch writes every chunk token's K/V row before the attention launch
+// reads them, so token t sees rows 0..pos0+t as in a decode step, and every token's arithmetic is
+// runq's (each sequence of the exact kernels is bit-identical to runq.c's forward): the K/V rows
+// are bit-identical to stepping through the prompt, and the weights are read once per 8 tokens
+// instead of once per token (src/llama.cpp:1029-1031 steps through the prompt).
+static int prefill_q8(thallama_decoder* d, int b, const int* tokens_h, int n, int pos0) {
+  if (!d->q8x || !d->pf_att || !d->pf_x) {
+    g_last_error = "thallama_decoder_prefill: int8 prefill needs the exact int8 kernels (group size 64)";
+    return (int)hipErrorNotSupported;
+  }
+  hipStream_t st = d->stream;
+  const long long kv_b_stride = (long long)d->L * d->S * d->kv_dim;
+  float* kc_b = d->s.key_cache + (long long)b * kv_b_stride;
+  float* vc_b = d->s.value_cache + (long long)b * kv_b_stride;
+  memcpy(d->pf_tok_h, tokens_h, sizeof(int) * n);
+  TL_TRY(hipMemcpyAsync(d->pf_tok, d->pf_tok_h, sizeof(int) * n, hipMemcpyHostToDevice, st));
+  for (int c = 0; c < n; c += kPrefillQ8Chunk) {
+    const int m = n - c < kPrefillQ8Chunk ? n - c : kPrefillQ8Chunk;
+    TL_TRY(tl::prefill_positions(d->pf_pos, pos0 + c, m, st));
+    const StepIO io{d->pf_x, d->pf_xb, d->pf_q, d->pf_hb, nullptr, kc_b, vc_b, 0, d->pf_tok + c, d->pf_pos, m,
+                    d->pf_att};
+    const int r = enqueue_step_io(d, io);
+    if (r) return r;
+  }
+  TL_TRY(hipStreamSynchronize(st));
+  return 0;
+}
+
 extern "C" int thallama_decoder_prefill(thallama_decoder* d, int b, const int* tokens_h, int n, int pos0) {
   if (!d || !tokens_h || n < 0 || b < 0 || b >= d->B || pos0 < 0 || pos0 + n > d->S) {
     g_last_error = "thallama_decoder_prefill: invalid argument";
     return (int)hipErrorInvalidValue;
   }
   if (n == 0) return 0;
-  if (d->q8 || !prefill_shape_ok(d)) {
-    g_last_error = "thallama_decoder_prefill: unsupported (int8 weights, or head size not 64/128/256)";
+  if (!prefill_shape_ok(d)) {
+    g_last_error = "thallama_decoder_prefill: unsupported (head size not 64/128/256)";
     return (int)hipErrorNotSupported;
   }
   for (int i = 0; i < n; ++i)
@@ -1464,6 +1516,7 @@ extern "C" int thallama_decoder_prefill(thallama_decoder* d, int b, const int* t
       g_last_error = "thallama_decoder_prefill: token out of range";
       return (int)hipErrorInvalidValue;
     }
+  if (d->q8) return prefill_q8(d, b, tokens_h, n, pos0);
   const int CH = kPrefillChunk, dim = d->dim, hid = d->hidden, kvd = d->kv_dim, S = d->S;
   const int max_ns = kPrefillMaxSplits;
   if (!d->pf_x) {

@@ -310,6 +310,103 @@ float* oracle_forward(OModel* m, int token, int pos) {
   return m->logits;
 }
 
+/* The same forward (seq.cpp:53-183) with every accumulation, product, norm, softmax and SwiGLU in
+ * double precision: the exact value of the reference's arithmetic up to ~1e-16, used only to
+ * attribute a GPU-vs-CPU logit difference (which side carries the rounding error).  Reads the
+ * fp32 weights and the K/V rows 0..pos-1 of m's cache (as float); the current position's K/V
+ * are kept in double and m is not modified.  The RoPE (cos, sin) are the reference's float values
+ * (powf/cosf/sinf of the float angle, seq.cpp:88-92): parameters, not accumulations. */
+static void matmul_f64(double* xout, const double* x, const float* w, int n, int d) {
+  int i;
+#pragma omp parallel for num_threads(g_threads) if (g_threads > 1 && (long)n * d > 65536) schedule(static)
+  for (i = 0; i < d; i++) {
+    double val = 0.0;
+    const float* wr = w + (size_t)i * n;
+    for (int j = 0; j < n; j++) val += (double)wr[j] * x[j];
+    xout[i] = val;
+  }
+}
+
+static void rmsnorm_f64(double* o, const double* x, const float* weight, int size) {
+  double ss = 0.0;
+  for (int j = 0; j < size; j++) ss += x[j] * x[j];
+  ss = 1.0 / sqrt(ss / size + (double)1e-5f);
+  for (int j = 0; j < size; j++) o[j] = (double)weight[j] * (ss * x[j]);
+}
+
+int oracle_forward_f64(OModel* m, int token, int pos, double* logits) {
+  const OCfg* p = &m->c;
+  const int dim = p->dim, hid = p->hidden_dim, hs = dim / p->n_heads;
+  const int kvd = (p->dim * p->n_kv_heads) / p->n_heads, kv_mul = p->n_heads / p->n_kv_heads;
+  const size_t big = (size_t)(hid > dim ? hid : dim);
+  double* x = (double*)malloc(sizeof(double) * dim);
+  double* xb = (double*)malloc(sizeof(double) * big);
+  double* xb2 = (double*)malloc(sizeof(double) * dim);
+  double* q = (double*)malloc(sizeof(double) * dim);
+  double* k = (double*)malloc(sizeof(double) * kvd);
+  double* v = (double*)malloc(sizeof(double) * kvd);
+  double* hb = (double*)malloc(sizeof(double) * hid);
+  double* hb2 = (double*)malloc(sizeof(double) * hid);
+  double* att = (double*)malloc(sizeof(double) * (pos + 1));
+  if (!x || !xb || !xb2 || !q || !k || !v || !hb || !hb2 || !att) return -1;
+  for (int i = 0; i < dim; i++) x[i] = m->emb[(size_t)token * dim + i];
+  for (int l = 0; l < p->n_layers; l++) {
+    const size_t L = l;
+    rmsnorm_f64(xb, x, m->rms_att + L * dim, dim);
+    matmul_f64(q, xb, m->wq + L * dim * dim, dim, dim);
+    matmul_f64(k, xb, m->wk + L * dim * kvd, dim, kvd);
+    matmul_f64(v, xb, m->wv + L * dim * kvd, dim, kvd);
+    for (int i = 0; i < dim; i += 2) {
+      const int head_dim = i % hs;
+      const float freq = 1.0f / powf(10000.0f, head_dim / (float)hs);
+      const float val = pos * freq;
+      const double fcr = cosf(val), fci = sinf(val);
+      for (int r = 0; r < (i < kvd ? 2 : 1); r++) {
+        double* vec = r == 0 ? q : k;
+        const double v0 = vec[i], v1 = vec[i + 1];
+        vec[i] = v0 * fcr - v1 * fci;
+        vec[i + 1] = v0 * fci + v1 * fcr;
+      }
+    }
+    const size_t loff = L * p->seq_len * (size_t)kvd;
+    for (int h = 0; h < p->n_heads; h++) {
+      const double* qh = q + h * hs;
+      const int off = (h / kv_mul) * hs;
+      double mx = -1e300, sum = 0.0;
+      for (int t = 0; t <= pos; t++) {
+        double sc = 0.0;
+        for (int i = 0; i < hs; i++)
+          sc += qh[i] * (t < pos ? (double)m->kc[loff + (size_t)t * kvd + off + i] : k[off + i]);
+        att[t] = sc / sqrt((double)hs);
+        if (att[t] > mx) mx = att[t];
+      }
+      for (int t = 0; t <= pos; t++) {
+        att[t] = exp(att[t] - mx);
+        sum += att[t];
+      }
+      double* o = xb + h * hs;
+      for (int i = 0; i < hs; i++) o[i] = 0.0;
+      for (int t = 0; t <= pos; t++) {
+        const double w = att[t] / sum;
+        for (int i = 0; i < hs; i++)
+          o[i] += w * (t < pos ? (double)m->vc[loff + (size_t)t * kvd + off + i] : v[off + i]);
+      }
+    }
+    matmul_f64(xb2, xb, m->wo + L * dim * dim, dim, dim);
+    for (int i = 0; i < dim; i++) x[i] += xb2[i];
+    rmsnorm_f64(xb, x, m->rms_ffn + L * dim, dim);
+    matmul_f64(hb, xb, m->w1 + L * dim * hid, dim, hid);
+    matmul_f64(hb2, xb, m->w3 + L * dim * hid, dim, hid);
+    for (int i = 0; i < hid; i++) hb[i] = hb[i] * (1.0 / (1.0 + exp(-hb[i]))) * hb2[i];
+    matmul_f64(xb, hb, m->w2 + L * dim * hid, hid, dim);
+    for (int i = 0; i < dim; i++) x[i] += xb[i];
+  }
+  rmsnorm_f64(xb, x, m->rms_final, dim);
+  matmul_f64(logits, xb, m->wcls, dim, p->vocab_size);
+  free(x); free(xb); free(xb2); free(q); free(k); free(v); free(hb); free(hb2); free(att);
+  return 0;
+}
+
 /* llama.cpp:275-286 */
 int oracle_argmax(const float* v, int n) {
   int max_i = 0;

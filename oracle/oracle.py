@@ -66,6 +66,7 @@ def lib():
             "oracle_write_v0": (C.c_int, [V, C.c_char_p]),
             "oracle_model_free": (None, [V]),
             "oracle_forward": (F, [V, C.c_int, C.c_int]),
+            "oracle_forward_f64": (C.c_int, [V, C.c_int, C.c_int, C.POINTER(C.c_double)]),
             "oracle_argmax": (C.c_int, [F, C.c_int]),
             "oracle_greedy": (C.c_int, [V, C.c_int, C.c_int, C.c_int, IP]),
             "oracle_q8_quantize": (None, [I8, F, F, C.c_int, C.c_int]),
@@ -195,6 +196,14 @@ class Model:
     def forward(self, token, pos):
         p = lib().oracle_forward(self.h, token, pos)
         return np.ctypeslib.as_array(p, shape=(self.vocab,)).copy()
+
+    def forward_f64(self, token, pos):
+        """The same forward in double precision from this model's K/V rows 0..pos-1 (the cache is
+        not modified): the exact value of the reference's arithmetic, to attribute rounding."""
+        out = np.zeros(self.vocab, np.float64)
+        if lib().oracle_forward_f64(self.h, token, pos, out.ctypes.data_as(C.POINTER(C.c_double))) != 0:
+            raise MemoryError("oracle_forward_f64")
+        return out
 
     def greedy(self, token, pos0, n):
         out = (C.c_int * n)()

@@ -43,7 +43,7 @@ def host(pkg):
     return H
 
 
-def expected_test_mode(host, ref, prompts, seq_len):
+def expected_test_mode(host, ref, prompts, seq_len, q8=False):
     tok = host.Tokenizer(TOK, V)
     outs, gen = [], 0
     for p in prompts:
@@ -51,7 +51,7 @@ def expected_test_mode(host, ref, prompts, seq_len):
         smp = host.Sampler(V, 1.0, 0.9, 314028)
         token, pos, text = ids[0], 0, b""
         while True:
-            lg = ref.forward(token, pos).astype(np.float32)
+            lg = (ref.q8_forward(token, pos) if q8 else ref.forward(token, pos)).astype(np.float32)
             nxt = ids[pos + 1] if pos < len(ids) - 1 else smp.sample(lg)
             pos += 1
             if nxt in (1, 2):
@@ -270,6 +270,41 @@ def test_gen_in_128_greedy_fixture(gpu, oracle, tmp_path, batch, n_prompts):
         else:
             rest = b""
     assert rest == b""
-    # the fixture has 137 greedy steps with a top-2 margin under 1e-4 (14 under 1e-5, one of
-    # 2.4e-7) over its 128 x 1023 steps: a handful of prompts may take the other branch
-    assert len(diverged) <= 16, diverged
+    # which prompts took the other branch, and where (printed and kept under gpurun_out/)
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", f"gen_in_128_diverged_b{batch}_n{n}.json"), "w") as f:
+        json.dump([{"prompt": i, "pos": p, "margin": m} for i, p, m in diverged], f)
+    print(f"diverged prompts (prompt, position, top-2 margin): {diverged}")
+    # the fixture has 137 greedy steps with a top-2 margin under 1e-4 and 14 under 1e-5 (one of
+    # 2.4e-7) over its 128 x 1023 steps: at most that many prompts may take the other branch
+    n_tight = sum(1 for ts in fx["near_ties"][:n] if any(t[1] < 1e-5 for t in ts))
+    assert len(diverged) <= n_tight, (n_tight, diverged)
+
+
+@pytest.mark.parametrize("prefill", [True, False])
+@pytest.mark.parametrize("batch", [1, 3])
+def test_test_mode_int8_prefill_byte_identical(gpu, host, model, tmp_path, batch, prefill):
+    """config[3]'s CLI path: a runq v2 int8 file in test mode.  Prompts go through the int8 prefill
+    (chunks of 8 tokens through the exact batched step) or, with THALLAMA_NO_PREFILL=1, one decode
+    step each like the reference (src/llama.cpp:1029-1031); the output file is the one the CPU
+    runq restatement samples either way (every int8 logit is bit-identical to runq's)."""
+    base, _ = model
+    ref = oracle_q8_of(base)
+    path = str(tmp_path / "model_q8.bin")
+    ref.write_v2(path)
+    inp = tmp_path / "in.txt"
+    inp.write_bytes((f"{len(PROMPTS)}\n" + "\n".join(PROMPTS) + "\n").encode())
+    out = tmp_path / "out.txt"
+    r = run_cli([path, "-m", "test", "-f", str(inp), "-o", str(out), "-b", str(batch), "-z", TOK], tmp_path,
+                env={"THALLAMA_NO_PREFILL": "0" if prefill else "1"})
+    want, gen = expected_test_mode(host, ref, PROMPTS, CFG[6], q8=True)
+    assert out.read_bytes() == f"{len(PROMPTS)}\n".encode() + b"".join(w + b"\n" for w in want)
+    assert f"Total achieved token: {gen}".encode() in r.stdout
+
+
+def oracle_q8_of(base):
+    """The int8 twin (runq.c restatement, group size 64) of the module's peaked fp32 model."""
+    import oracle as O
+    ref = O.Model(CFG, 0, payload=base.arena().copy())
+    ref.build_q8(64)
+    return ref

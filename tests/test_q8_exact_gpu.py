@@ -110,3 +110,45 @@ def test_forward_batch_c_abi_bitexact(gpu, oracle):
         for b in range(B):
             np.testing.assert_array_equal(bits(logits[b * cfg[5]:(b + 1) * cfg[5]]),
                                           bits(refs[b].q8_forward(int(toks[b, p]), p)), err_msg=f"b={b} pos={p}")
+
+
+@pytest.mark.parametrize("cfg", [SMALL, HEAD128])
+@pytest.mark.parametrize("B,persistent", [(1, 1), (1, 0), (3, 0)])
+@pytest.mark.parametrize("n", [1, 7, 8, 21])
+def test_int8_prefill_bitexact(gpu, oracle, cfg, B, persistent, n):
+    """int8 prefill (thallama_decoder_prefill on an int8 decoder: chunks of up to 8 prompt tokens
+    through the exact batched step) leaves slot b's K/V rows as stepping through the prompt would:
+    the next forward's logits equal runq's after feeding the prompt one token at a time, bit for
+    bit, and so do the following greedy steps."""
+    c = gpu.Config.make(*cfg)
+    m = gpu.DeviceModel(c, 0, seed=31)
+    q = gpu.DeviceModelQ8(c, 0, 64, from_model=m)
+    state = gpu.DeviceState(c, B)
+    dec = gpu.Decoder(q, state)
+    dec.set(gpu.OPT_PERSISTENT, persistent)
+    rng = np.random.default_rng(7 + n + B)
+    prompt = [int(t) for t in rng.integers(0, cfg[5], n + 1)]
+    slot = B - 1
+    pos0 = 3 if B > 1 else 0
+    ref = oracle.Model(cfg, 0, seed=31)
+    ref.build_q8(64)
+    if pos0:  # slot's earlier rows, by decode steps on both sides
+        pre = [int(t) for t in rng.integers(0, cfg[5], pos0)]
+        for p, t in enumerate(pre):
+            ref.q8_forward(t, p)
+            tk = [0] * B
+            ps = [0] * B
+            tk[slot], ps[slot] = t, p
+            dec.forward(tk, ps, want_logits=False)
+    assert dec.prefill(slot, prompt[:n], pos0) == 0, gpu.lib().thallama_last_error()
+    for p, t in enumerate(prompt[:n]):
+        ref.q8_forward(t, pos0 + p)
+    tok, pos = prompt[n], pos0 + n
+    for step in range(4):
+        want = ref.q8_forward(tok, pos)
+        tk = [0] * B
+        ps = [0] * B
+        tk[slot], ps[slot] = tok, pos
+        got = dec.forward(tk, ps)[slot]
+        np.testing.assert_array_equal(bits(got), bits(want), err_msg=f"step {step} after a {n}-token prefill")
+        tok, pos = int(np.argmax(want)), pos + 1
