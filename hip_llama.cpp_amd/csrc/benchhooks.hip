@@ -6,7 +6,6 @@
 #include <vector>
 #include "../../include/thallama.h"
 #include "gemv_dispatch.hpp"
-#include "gemv_mb.hpp"
 
 __global__ void __launch_bounds__(256) k_bench_fill(float* d, size_t n, uint32_t seed, float scale) {
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
@@ -33,8 +32,6 @@ extern "C" int thallama_gemv_bench(int mode, int M, int K, int nb, int ipw, int 
   int* pos = nullptr;
   float *xn = nullptr, *mpart = nullptr;
   unsigned* mcnt = nullptr;
-  float* mbpart = nullptr;
-  unsigned* mbcnt = nullptr;
   float2* rope = nullptr;
   hipStream_t s = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -61,9 +58,6 @@ extern "C" int thallama_gemv_bench(int mode, int M, int K, int nb, int ipw, int 
     CK(hipMalloc(&mpart, (size_t)tl::mfma_target_blocks() * 2 * 256 * 4));
     CK(hipMalloc(&mcnt, (size_t)tl::mfma_target_blocks() * 4));
     CK(hipMemsetAsync(mcnt, 0, (size_t)tl::mfma_target_blocks() * 4, s));
-    CK(hipMalloc(&mbpart, (size_t)4 << 22));
-    CK(hipMalloc(&mbcnt, (size_t)32768 * 4));
-    CK(hipMemsetAsync(mbcnt, 0, (size_t)32768 * 4, s));
   }
   {
     tl::GemvParams p = {};
@@ -87,10 +81,6 @@ extern "C" int thallama_gemv_bench(int mode, int M, int K, int nb, int ipw, int 
     p.xn = xn;
     p.mpart = mpart;
     p.mcnt = mcnt;
-    p.mbpart = mbpart;
-    p.mbcnt = mbcnt;
-    p.mbpart_floats = mbpart ? 4LL << 20 : 0;
-    p.mbcnt_n = mbcnt ? 32768 : 0;
     tl::GemvCfg c;
     c.ipw = ipw;
     c.waves = waves;
@@ -117,7 +107,7 @@ done:
   (void)hipStreamSynchronize(s);
   (void)hipFree(W); (void)hipFree(x); (void)hipFree(rw); (void)hipFree(y); (void)hipFree(kc); (void)hipFree(vc);
   (void)hipFree(pos); (void)hipFree(rope);
-  (void)hipFree(xn); (void)hipFree(mpart); (void)hipFree(mcnt); (void)hipFree(mbpart); (void)hipFree(mbcnt);
+  (void)hipFree(xn); (void)hipFree(mpart); (void)hipFree(mcnt);
   (void)hipEventDestroy(e0); (void)hipEventDestroy(e1); (void)hipStreamDestroy(s);
 #undef CK
   return (int)err;
@@ -173,53 +163,5 @@ extern "C" int thallama_seqsum_time(const float* in_d, int n, int count, float* 
   hipLaunchKernelGGL(k_seqsum_time, dim3(count), dim3(64), lds, 0, in_d, n, out_d, cyc_d);
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipDeviceSynchronize();
-  return (int)e;
-}
-
-extern "C" int thallama_gemv_check(int mode, int M, int K, int nb, const float* W0, const float* W1, const float* x,
-                                   const float* rms_w, float* y, const int* pos, int has_pos, long long y_stride,
-                                   int use_mb, int* took_mb) {
-  if (mode < tl::GM_STORE || mode > tl::GM_SWIGLU || M <= 0 || K <= 0 || nb <= 0 || !W0 || !x || !y) return (int)hipErrorInvalidValue;
-  if (mode == tl::GM_SWIGLU && !W1) return (int)hipErrorInvalidValue;
-  float* mbpart = nullptr;
-  unsigned* mbcnt = nullptr;
-  const long long nparts = 4LL << 20;
-  const int ncnt = M / 4 + 64;
-  hipError_t e = hipSuccess;
-  tl::GemvParams p = {};
-  p.W0 = W0;
-  p.W1 = W1;
-  p.K = K;
-  p.n_items = M;
-  p.nb = nb;
-  p.x = x;
-  p.x_stride = K;
-  p.rms_w = rms_w;
-  p.y = y;
-  p.y_stride = y_stride;
-  p.has_pos = has_pos;
-  p.pos = pos;
-  if (use_mb) {
-    if ((e = hipMalloc(&mbpart, sizeof(float) * nparts)) != hipSuccess) goto out;
-    if ((e = hipMalloc(&mbcnt, sizeof(unsigned) * ncnt)) != hipSuccess) goto out;
-    if ((e = hipMemset(mbcnt, 0, sizeof(unsigned) * ncnt)) != hipSuccess) goto out;
-    p.mbpart = mbpart;
-    p.mbcnt = mbcnt;
-    p.mbpart_floats = nparts;
-    p.mbcnt_n = ncnt;
-  }
-  tl::mb_override() = use_mb ? 8 : 0;
-  if (took_mb) {
-    tl::MbGeom g;
-    size_t lds = 0;
-    *took_mb = mode == tl::GM_STORE ? tl::mb_plan<tl::GM_STORE>(p, g, lds)
-             : mode == tl::GM_RESID ? tl::mb_plan<tl::GM_RESID>(p, g, lds) : tl::mb_plan<tl::GM_SWIGLU>(p, g, lds);
-  }
-  if ((e = tl::launch_gemv(mode, p, nullptr, true)) != hipSuccess) goto out;
-  e = hipDeviceSynchronize();
-out:
-  tl::mb_override() = -1;
-  (void)hipFree(mbpart);
-  (void)hipFree(mbcnt);
   return (int)e;
 }

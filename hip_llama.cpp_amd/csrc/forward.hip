@@ -149,15 +149,8 @@ struct thallama_decoder {
   bool ssq_carry = false;       // this step carries them (ssq_carry_ok)
   signed char* xq_d = nullptr;  // int8 batched: activations quantised once per launch [8][max(dim, hidden)]
   float* xqs_d = nullptr;       //   and their group scales
-  signed char* hq_d = nullptr;  // int8 4..8 sequences: SwiGLU output quantised for W2 [8][hidden]
-  float* hqs_d = nullptr;       //   its group scales
-  unsigned* hcnt_d = nullptr;   //   and one ticket per 64-row group (zero between launches)
   float* mpart_d = nullptr;     // matrix-core GEMV split-K partial tiles
   unsigned* mcnt_d = nullptr;   //   and their tickets
-  float* mbpart_d = nullptr;    // 4x4x1 matrix-core GEMV (gemv_mb.hpp): partial-tile slabs
-  unsigned* mbcnt_d = nullptr;  //   and one ticket per 4-row group
-  long long mbpart_n = 0;
-  int mbcnt_n = 0;
   float* part_d = nullptr;      // attention partials [B][H][<=16 units][hs+4]
   unsigned* cnt_d = nullptr;    // attention combine tickets [B][H]
   bool q8 = false;              // int8 (runq Q8_0) weights in w8; w then holds only norms + embedding
@@ -361,13 +354,6 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
     TL_TRY(hipMalloc(&d->mpart_d, sizeof(float) * nblk * 2 * 256));
     TL_TRY(hipMalloc(&d->mcnt_d, sizeof(unsigned) * nblk));
     TL_TRY(hipMemset(d->mcnt_d, 0, sizeof(unsigned) * nblk));
-    int rows = d->V > d->hidden ? d->V : d->hidden;
-    rows = rows > d->dim + 2 * d->kv_dim ? rows : d->dim + 2 * d->kv_dim;
-    d->mbcnt_n = rows / 4 + 64;
-    d->mbpart_n = 4LL << 20;
-    TL_TRY(hipMalloc(&d->mbpart_d, sizeof(float) * (size_t)d->mbpart_n));
-    TL_TRY(hipMalloc(&d->mbcnt_d, sizeof(unsigned) * (size_t)d->mbcnt_n));
-    TL_TRY(hipMemset(d->mbcnt_d, 0, sizeof(unsigned) * (size_t)d->mbcnt_n));
   }
   {
     const size_t nsmax = (size_t)((d->S + kAttnChunk - 1) / kAttnChunk);
@@ -453,12 +439,7 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   (void)hipFree(d->xq_d);
   (void)hipFree(d->q8att_d);
   (void)hipFree(d->xqs_d);
-  (void)hipFree(d->hq_d);
-  (void)hipFree(d->hqs_d);
-  (void)hipFree(d->hcnt_d);
   (void)hipFree(d->mcnt_d);
-  (void)hipFree(d->mbpart_d);
-  (void)hipFree(d->mbcnt_d);
   (void)hipFree(d->part_d);
   (void)hipFree(d->cnt_d);
   (void)hipFree(d->psync);
@@ -499,10 +480,6 @@ static hipError_t gemv(thallama_decoder* d, int mode, tl::GemvParams& p, const Q
   if (!d->q8) {
     p.mpart = d->mpart_d;
     p.mcnt = d->mcnt_d;
-    p.mbpart = d->mbpart_d;
-    p.mbcnt = d->mbcnt_d;
-    p.mbpart_floats = d->mbpart_n;
-    p.mbcnt_n = d->mbcnt_n;
     return tl::launch_gemv(mode, p, d->stream, d->nt);
   }
   p.Q0 = t0 ? t0->q : nullptr;
@@ -529,18 +506,6 @@ static int q8_attn_quant(const thallama_decoder* d) {
          (d->hs == 64 || d->hs == 128 || d->hs == 256) && (d->dim % 64) == 0;
 }
 
-// int8 decoder, 4..8 sequences on the matrix-core kernel: the W1/W3 + SwiGLU launch stores its
-// output quantised as well (gemv_q8_mfma.hpp), so W2 skips its quantise pass.  Opt-in
-// (THALLAMA_Q8_FFN_QUANT=1): the group hand-off (write-through, ticket, read-back) adds ~5 us
-// to the SwiGLU launch's tail, about what the skipped 4.8 us pass saved.
-static int q8_ffn_quant(const thallama_decoder* d) {
-  static const bool on = [] {
-    const char* e = getenv("THALLAMA_Q8_FFN_QUANT");
-    return e && atoi(e) != 0;
-  }();
-  return on && d->q8 && !d->q8x && tl::q8_swiglu_quant_ok(d->B, d->w8.group_size, d->dim, d->hidden);
-}
-
 // Enqueue one decode step reading tok_d / pos_d; logits land in s.logits.
 // fp32 batched steps on the matrix cores: the residual launches (Wo, W2) leave per-tile sums of
 // squares of the residual stream and the next normed launch reduces them instead of running a
@@ -552,7 +517,6 @@ static int q8_ffn_quant(const thallama_decoder* d) {
 // matrix path ignore ssq_in (the streaming kernels normalise from x).
 static bool ssq_carry_ok(const thallama_decoder* d) {
   if (d->q8 || !d->ssq_d || d->no_ssq || (d->dim + 15) / 16 > 256) return false;  // (the kernel sums <= 256 tiles)
-  if (d->mbpart_d && tl::gemv_mb_takes(d->B)) return false;  // gemv_mb.hpp normalises in-block, keeps no sums
   for (int l = 0; l < d->L; ++l) {
     tl::GemvParams wo = {}, w2 = {};
     wo.W0 = d->w.wo + (long long)l * d->dim * d->dim;
@@ -732,11 +696,6 @@ static int enqueue_step_io(thallama_decoder* d, const StepIO& io) {
       norm_from_ssq(d, p);
       p.y = io.hb;
       p.y_stride = hid;
-      if (d->hq_d) {
-        p.yq = d->hq_d;
-        p.yqs = d->hqs_d;
-        p.gcnt = d->hcnt_d;
-      }
       int ev = prof_begin(d);
       TL_TRY(gemv(d, tl::GM_SWIGLU, p, Q8L(w1), Q8L(w3), nullptr));
       prof_end(d, THALLAMA_K_FFN_UP, ev);
@@ -752,11 +711,6 @@ static int enqueue_step_io(thallama_decoder* d, const StepIO& io) {
       p.x_stride = hid;
       p.y = io.x;
       p.y_stride = dim;
-      if (d->hq_d) {
-        p.xq = d->hq_d;
-        p.xqs = d->hqs_d;
-        p.xq_ready = 1;
-      }
       ssq_to_next_norm(d, p);
       int ev = prof_begin(d);
       TL_TRY(gemv(d, tl::GM_RESID, p, Q8L(w2), nullptr, nullptr));
@@ -1372,12 +1326,6 @@ extern "C" int thallama_decoder_create_q8(thallama_decoder** out, const Config* 
     const size_t kmax = (size_t)(d->dim > d->hidden ? d->dim : d->hidden);
     TL_TRY(hipMalloc(&d->xq_d, 8 * kmax));
     TL_TRY(hipMalloc(&d->xqs_d, sizeof(float) * 8 * (kmax / 16 + 1)));
-    if (q8_ffn_quant(d)) {
-      TL_TRY(hipMalloc(&d->hq_d, 8 * (size_t)d->hidden));
-      TL_TRY(hipMalloc(&d->hqs_d, sizeof(float) * 8 * (size_t)(d->hidden / 64)));
-      TL_TRY(hipMalloc(&d->hcnt_d, sizeof(unsigned) * (size_t)(d->hidden / 64)));
-      TL_TRY(hipMemset(d->hcnt_d, 0, sizeof(unsigned) * (size_t)(d->hidden / 64)));
-    }
   }
   if (batch > 1 && d->pok) {  // the batched persistent step is fp32 only: int8 batches run multi-launch
     d->pok = false;

@@ -20,8 +20,6 @@ bool gemv_fast_ok(const GemvParams& p) {
 
 bool gemv_matrix_path(const GemvParams& p) { return matrix_path_ok(p); }
 
-bool gemv_mb_takes(int nb) { return nb >= 2 && nb <= 8 && nb <= mb_max_nb(); }
-
 // Measured on MI355X (profiles/r01_gemv_sweep.json, llama2-7B shapes, weights streamed
 // from HBM): prefetch-before-staging costs 64 VGPRs and loses occupancy everywhere
 // (-2..-12 %); non-temporal weight loads win 5-10 %; at NB = 1 one item per wave is

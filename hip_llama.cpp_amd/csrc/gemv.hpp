@@ -74,11 +74,6 @@ struct GemvParams {
   signed char* xq;
   float* xqs;
   int xq_ready;  // xq/xqs already hold this launch's quantised activations (attention wrote them)
-  // int8 matrix-core SwiGLU launch only: also store the output quantised for W2 ([nb][n_items]
-  // codes, [nb][n_items/64] scales; n_items % 64 == 0), with one zeroed ticket per 64-row group
-  signed char* yq;
-  float* yqs;
-  unsigned* gcnt;
   // optional split-K scratch for the matrix-core path: per-block partial tiles
   // [tiles][splits][2][256] and one ticket per tile (zero between launches)
   float* mpart;
@@ -91,12 +86,6 @@ struct GemvParams {
   float* ssq_out;
   const float* ssq_in;
   int ssq_nt;            // tiles of the producing launch (its rows / 16)
-  // optional scratch of the 4x4x1 matrix-core path (gemv_mb.hpp): partial-tile slabs of row groups
-  // cut between waves, and one ticket per 4-row group (zero between launches)
-  float* mbpart;
-  unsigned* mbcnt;
-  long long mbpart_floats;
-  int mbcnt_n;
 };
 
 // Blocks the matrix-core GEMV aims for: kMfmaDepth per CU (env THALLAMA_MFMA_DEPTH).

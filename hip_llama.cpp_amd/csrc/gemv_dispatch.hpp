@@ -30,11 +30,6 @@ bool gemv_fast_ok(const GemvParams& p);
 // this (launch_mode and forward.hip both call it; gemv_launch.hpp matrix_path_ok).
 bool gemv_matrix_path(const GemvParams& p);
 
-// True when launches of nb sequences may take the 4x4x1 matrix-core stream (gemv_mb.hpp), which
-// normalises from the staged activations itself and neither reads ssq_in nor writes ssq_out: a
-// decoder of that batch carries no sums (its normed launches that fall back run the prologue).
-bool gemv_mb_takes(int nb);
-
 // Enqueue y = W x' for p.nb sequences on `stream` with epilogue `mode`.
 hipError_t launch_gemv(int mode, const GemvParams& p, hipStream_t stream, bool nt);
 hipError_t launch_gemv_cfg(int mode, const GemvParams& p, hipStream_t stream, const GemvCfg& cfg);

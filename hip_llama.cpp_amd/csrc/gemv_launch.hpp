@@ -3,7 +3,6 @@
 #pragma once
 #include <stdlib.h>
 #include "gemv_dispatch.hpp"
-#include "gemv_mb.hpp"
 #include "gemv_mfma.hpp"
 #include "gemv_rr.hpp"
 
@@ -147,15 +146,6 @@ inline hipError_t launch_mode(const GemvParams& p0, hipStream_t s, const GemvCfg
       if (p.vc) p.vc += (long long)b0 * p.kv_b_stride;
     }
     hipError_t e;
-    if (!cfg) {  // 2..8 sequences: the 4x4x1 matrix-core stream (gemv_mb.hpp) when it takes the shape
-      MbGeom g;
-      size_t lds = 0;
-      if (mb_plan<MODE>(p, g, lds)) {
-        e = mb_launch<MODE>(p, g, lds, s, nt);
-        if (e != hipSuccess) return e;
-        continue;
-      }
-    }
     const GemvCfg c = cfg ? *cfg : gemv_default_cfg(MODE, p.n_items, p.K, p.nb, nt);
     const bool matrix = !cfg && matrix_path_ok(p) &&
                         ((!p.rms_w && !p.tok) || p.xn || (p.rms_w && p.ssq_in && !p.tok));

@@ -191,8 +191,7 @@ __global__ void __launch_bounds__(kMfmaWaves * 64) gemv_q8_mfma_kernel(GemvParam
     const int R = tile * 16 + row;
     if (j < nb && R < n_rows) {
       if constexpr (MODE == GM_SWIGLU) {
-        if (p.yq) st1_sc1(p.y + (long long)j * p.y_stride + R, silu_mul(tot(0, t), tot(NR - 1, t)));
-        else epi_one<MODE>(p, R, j, tot(0, t), tot(NR - 1, t));
+        epi_one<MODE>(p, R, j, tot(0, t), tot(NR - 1, t));
       } else if constexpr (MODE == GM_QKV) {
         if ((row & 1) == 0) epi_one<MODE>(p, R >> 1, j, tot(0, t), tot(0, t + 16));
       } else {
@@ -201,29 +200,6 @@ __global__ void __launch_bounds__(kMfmaWaves * 64) gemv_q8_mfma_kernel(GemvParam
     }
   }
   if (msplit > 1 && threadIdx.x == 0) __hip_atomic_store(p.mcnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if constexpr (MODE == GM_SWIGLU) {
-    // W2's input quantised here (p.yq): the last of the four tiles of a 64-row group to finish
-    // reads the group's SwiGLU outputs back (written through above) and applies runq's
-    // quantisation per sequence (one wave per sequence, one lane per row) - the arithmetic of
-    // gemv_q8_prequant_kernel on the same floats, so W2 skips its quantise launch
-    if (p.yq) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      const int grp = tile >> 2;
-      if (threadIdx.x == 0)
-        s_last = __hip_atomic_fetch_add(p.gcnt + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3u;
-      __syncthreads();
-      if (!s_last) return;
-      const int R = grp * 64 + lane;
-      for (int j = wave; j < nb; j += W) {
-        const float v = ld1_sc1(p.y + (long long)j * p.y_stride + R);
-        const float scale = __fdiv_rn(wave_max_u(fabsf(v)), 127.0f);
-        p.yq[(long long)j * n_rows + R] = (signed char)q8_code(v, scale);
-        if (lane == 0) p.yqs[(long long)j * (n_rows >> 6) + grp] = scale;
-      }
-      if (threadIdx.x == 0) __hip_atomic_store(p.gcnt + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 }  // namespace tl

@@ -26,12 +26,6 @@ static bool q8_mfma_enabled() {
   return v;
 }
 
-// Whether a GM_SWIGLU launch of this shape takes the int8 matrix-core kernel and so can store its
-// output quantised for W2 (GemvParams::yq).
-bool q8_swiglu_quant_ok(int nb, int gs, int K, int n_items) {
-  return nb >= 4 && nb <= 8 && gs == 64 && (K & 255) == 0 && (n_items & 63) == 0 && q8_mfma_enabled();
-}
-
 bool gemv_q8_fast_ok(const GemvParams& p) {
   if (p.K <= 0 || p.gs < 32 || p.gs > 128 || (p.gs & (p.gs - 1)) || p.K % p.gs || (p.K & 15)) return false;
   const void* ptrs[] = {p.Q0, p.Q1, p.Q2, p.x, p.emb, p.rms_w};
@@ -125,7 +119,6 @@ template <int MODE>
 static hipError_t launch_q8_mode(const GemvParams& p0, hipStream_t s, bool nt) {
   if (p0.n_items <= 0 || p0.nb <= 0) return hipSuccess;
   if (!gemv_q8_fast_ok(p0)) {
-    if (p0.yq) return hipErrorInvalidValue;
     hipLaunchKernelGGL((gemv_q8_generic_kernel<MODE>), dim3((p0.n_items + 3) / 4, p0.nb), dim3(256), 0, s, p0);
     return hipGetLastError();
   }
@@ -160,9 +153,6 @@ static hipError_t launch_q8_mode(const GemvParams& p0, hipStream_t s, bool nt) {
     } else {
       p.xq = nullptr;
     }
-    if (p.yq && !(MODE == GM_SWIGLU && p0.nb <= 8 && p.nb >= 4 && p.xq && p.gs == 64 && (p.K & 255) == 0 &&
-                  (p.n_items & 63) == 0 && q8_mfma_enabled()))
-      return hipErrorInvalidValue;  // the caller must know the output quantisation is done
     if (p.nb >= 4 && p.xq && p.gs == 64 && (p.K & 255) == 0 && q8_mfma_enabled()) {
       // 4..8 sequences: the int8 matrix-core kernel (gemv_q8_mfma.hpp), K split across blocks
       // like the fp32 one (in 256-byte runs)

@@ -7,7 +7,6 @@ namespace tl {
 bool gemv_q8_fast_ok(const GemvParams& p);
 // Enqueue the Q8_0 GEMV with epilogue `mode`; p.Q*/p.S*/p.gs describe the weights.
 hipError_t launch_gemv_q8(int mode, const GemvParams& p, hipStream_t stream, bool nt);
-bool q8_swiglu_quant_ok(int nb, int gs, int K, int n_items);
 // The int8 step in runq's arithmetic order for 1..8 sequences (q8_exact.hip): shape check, the
 // GEMV (quantises its input first unless p.xq_ready; p.xq / p.xqs scratch required) and the
 // attention (scores through att [B][H][S], output fp32 into a.out).

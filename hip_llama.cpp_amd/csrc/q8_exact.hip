@@ -276,7 +276,7 @@ static hipError_t launch_q8x_w(const GemvParams& p, hipStream_t s, size_t lds) {
 template <int MODE>
 static hipError_t launch_q8x_mode(const GemvParams& p0, hipStream_t s, bool nt) {
   if (p0.n_items <= 0 || p0.nb <= 0) return hipSuccess;
-  if (p0.nb > 8 || !p0.xq || !p0.xqs || p0.yq) return hipErrorInvalidValue;
+  if (p0.nb > 8 || !p0.xq || !p0.xqs) return hipErrorInvalidValue;
   GemvParams p = p0;
   if (!p.xq_ready) {
     const size_t lds = p.rms_w ? (size_t)64 * (4 * ((p.K + 255) >> 8) + 4) * 4 : 0;  // seqsum_floats(K)

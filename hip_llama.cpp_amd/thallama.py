@@ -180,7 +180,6 @@ def lib():
             "thallama_memset": (I, [VP, I, S]),
             "thallama_sync": (I, []),
             "thallama_seqsum_check": (I, [VP, I, I, VP]),
-            "thallama_gemv_check": (I, [I, I, I, I, VP, VP, VP, VP, VP, VP, I, C.c_longlong, I, c_int_p]),
             "thallama_seqsum_time": (I, [VP, I, I, VP, VP]),
             "thallama_last_error": (C.c_char_p, []),
         }

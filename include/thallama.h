@@ -146,15 +146,6 @@ double thallama_step_bytes(const Config* cfg, int batch, int kclass, const int* 
 int thallama_gemv_bench(int mode, int M, int K, int nb, int ipw, int waves, int pf, int nt, int iters,
                         double* us_out);
 
-/* Test hook: one batched GEMV launch through the library's dispatcher on caller device buffers
- * (synchronous).  mode 0 store (y[b*y_stride + has_pos*pos[b] + r]), 1 residual (y[b*y_stride + r]
- * += ...), 2 SwiGLU (W0 = W1, W1 = W3); rows M, row length K, nb sequences of x[nb][K], optional
- * RMSNorm weights rms_w.  use_mb = 0 withholds the scratch of the 4x4x1 matrix-core stream
- * (csrc/gemv_mb.hpp); *took_mb says whether that kernel took the launch. */
-int thallama_gemv_check(int mode, int M, int K, int nb, const float* W0, const float* W1, const float* x,
-                        const float* rms_w, float* y, const int* pos, int has_pos, long long y_stride,
-                        int use_mb, int* took_mb);
-
 /* Test hook: the wave-parallel left-to-right fp32 sum (csrc/seqsum.hpp) of `count` arrays of n
  * floats (device in_d, n <= 8192) into out_d[count]; synchronous. */
 int thallama_seqsum_check(const float* in_d, int n, int count, float* out_d);
