@@ -19,6 +19,7 @@
 #include <math.h>
 #include <string.h>
 #include <atomic>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -141,6 +142,11 @@ struct thallama_decoder {
   int* pos_h = nullptr;
   int* nxt_h = nullptr;  // pinned: argmax ids of a greedy step
   unsigned* perr_h = nullptr;  // pinned: the persistent step's error word, read back on d->stream
+  hipEvent_t ev_stage = nullptr;  // pipeline stage done (thallama_decoder_stage)
+  // layer streaming (thaDNN_s_forward_70B): the H2D copy stream and, per staging slot, layer
+  // copied / layer consumed events
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_used[2] = {nullptr, nullptr};
   bool err_pending = false;    // perr_h holds the word of launches not yet checked
   float2* rope_d = nullptr;
   float* xn_d = nullptr;        // [<=16][dim] normed rows for the matrix-core GEMV (batch >= 2)
@@ -390,6 +396,7 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
     TL_TRY(hipMemset(d->mcnt_d, 0, sizeof(unsigned) * nblk));
   }
   TL_TRY(hipHostMalloc(&d->perr_h, sizeof(unsigned), hipHostMallocDefault));
+  TL_TRY(hipEventCreateWithFlags(&d->ev_stage, hipEventDisableTiming));
   *d->perr_h = 0;
   if (prefill_shape_ok(d)) {  // batched prompt processing (thallama_decoder_prefill)
     const size_t CH = kPrefillChunk, dim = d->dim, hid = d->hidden;
@@ -424,6 +431,12 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   ApiLock lock(api_mu());
   drop_graphs(d);
   for (auto e : d->ev_pool) (void)hipEventDestroy(e);
+  if (d->ev_stage) (void)hipEventDestroy(d->ev_stage);
+  for (int i = 0; i < 2; ++i) {
+    if (d->ev_copied[i]) (void)hipEventDestroy(d->ev_copied[i]);
+    if (d->ev_used[i]) (void)hipEventDestroy(d->ev_used[i]);
+  }
+  if (d->copy_stream) (void)hipStreamDestroy(d->copy_stream);
   (void)hipFree(d->tok_d);
   (void)hipFree(d->pos_d);
   (void)hipFree(d->out_d);
@@ -541,6 +554,11 @@ static void norm_from_ssq(const thallama_decoder* d, tl::GemvParams& p) {
 // Where a multi-launch step reads and writes: the decoder's RunState for its B sequences, or
 // (prefill) a chunk of one sequence's prompt tokens as nb "sequences" at their own positions over
 // that sequence's cache (kv_b_stride 0), with no classifier.
+// One layer's fp32 weights.
+struct LayerW {
+  const float *rms_att, *wq, *wk, *wv, *wo, *rms_ffn, *w1, *w2, *w3;
+};
+
 struct StepIO {
   float *x, *xb, *q, *hb, *logits;  // logits == nullptr: layers only
   float *kc, *vc;
@@ -548,6 +566,11 @@ struct StepIO {
   int *tok, *pos;
   int nb;
   float* att;  // int8 exact attention scores [nb][H][S]
+  bool embed = true;  // layer 0 reads the tokens' embedding rows (false: x already holds the input)
+  // layer-streamed weights (thaDNN_s_forward_70B): layer l's pointers and the stream work around
+  // it; null: the decoder's own TransformerWeights
+  std::function<LayerW(int)> layer_w;
+  std::function<int(int)> before_layer, after_layer;
 };
 
 static StepIO step_io(thallama_decoder* d) {
@@ -556,28 +579,40 @@ static StepIO step_io(thallama_decoder* d) {
                 d->tok_d, d->pos_d, d->B, d->q8att_d};
 }
 
+static LayerW layer_of(const TransformerWeights& w, int l, long long dim, long long kvd, long long hid) {
+  const long long ll = l;
+  return LayerW{w.rms_att_weight + ll * dim, w.wq + ll * dim * dim, w.wk + ll * dim * kvd, w.wv + ll * dim * kvd,
+                w.wo + ll * dim * dim, w.rms_ffn_weight + ll * dim, w.w1 + ll * dim * hid, w.w2 + ll * dim * hid,
+                w.w3 + ll * dim * hid};
+}
+
 static int enqueue_step_io(thallama_decoder* d, const StepIO& io) {
   const int dim = d->dim, hid = d->hidden, kvd = d->kv_dim, S = d->S;
   const long long kv_b_stride = io.kv_b_stride;
   const TransformerWeights& w = d->w;
-  d->ssq_carry = ssq_carry_ok(d) && io.nb == d->B;
+  d->ssq_carry = ssq_carry_ok(d) && io.nb == d->B && !io.layer_w && io.embed;
   for (int l = 0; l < d->L; ++l) {
     const long long ll = l;
+    if (io.before_layer) {
+      const int r = io.before_layer(l);
+      if (r) return r;
+    }
+    const LayerW lw = io.layer_w ? io.layer_w(l) : layer_of(w, l, dim, kvd, hid);
     // 1. QKV (+ embedding at layer 0)
     {
       tl::GemvParams p = {};
-      p.W0 = w.wq + ll * dim * dim;
-      p.W1 = w.wk + ll * dim * kvd;
-      p.W2 = w.wv + ll * dim * kvd;
+      p.W0 = lw.wq;
+      p.W1 = lw.wk;
+      p.W2 = lw.wv;
       p.K = dim;
       p.n_items = (dim + 2 * kvd) / 2;
       p.nb = io.nb;
       p.x = io.x;
       p.x_stride = dim;
-      p.rms_w = w.rms_att_weight + ll * dim;
+      p.rms_w = lw.rms_att;
       p.xn = d->xn_d;
       if (l > 0) norm_from_ssq(d, p);
-      if (l == 0) {
+      if (l == 0 && io.embed) {
         p.tok = io.tok;
         p.emb = w.token_embedding_table;
         p.x_out = io.x;
@@ -667,7 +702,7 @@ static int enqueue_step_io(thallama_decoder* d, const StepIO& io) {
     // 3. Wo + residual
     {
       tl::GemvParams p = {};
-      p.W0 = w.wo + ll * dim * dim;
+      p.W0 = lw.wo;
       p.K = dim;
       p.n_items = dim;
       p.nb = io.nb;
@@ -684,14 +719,14 @@ static int enqueue_step_io(thallama_decoder* d, const StepIO& io) {
     // 4. RMSNorm(ffn) + W1/W3 + SwiGLU
     {
       tl::GemvParams p = {};
-      p.W0 = w.w1 + ll * dim * hid;
-      p.W1 = w.w3 + ll * dim * hid;
+      p.W0 = lw.w1;
+      p.W1 = lw.w3;
       p.K = dim;
       p.n_items = hid;
       p.nb = io.nb;
       p.x = io.x;
       p.x_stride = dim;
-      p.rms_w = w.rms_ffn_weight + ll * dim;
+      p.rms_w = lw.rms_ffn;
       p.xn = d->xn_d;
       norm_from_ssq(d, p);
       p.y = io.hb;
@@ -703,7 +738,7 @@ static int enqueue_step_io(thallama_decoder* d, const StepIO& io) {
     // 5. W2 + residual
     {
       tl::GemvParams p = {};
-      p.W0 = w.w2 + ll * dim * hid;
+      p.W0 = lw.w2;
       p.K = hid;
       p.n_items = dim;
       p.nb = io.nb;
@@ -715,6 +750,10 @@ static int enqueue_step_io(thallama_decoder* d, const StepIO& io) {
       int ev = prof_begin(d);
       TL_TRY(gemv(d, tl::GM_RESID, p, Q8L(w2), nullptr, nullptr));
       prof_end(d, THALLAMA_K_FFN_DOWN, ev);
+    }
+    if (io.after_layer) {
+      const int r = io.after_layer(l);
+      if (r) return r;
     }
   }
   // final RMSNorm + classifier
@@ -729,7 +768,7 @@ static int enqueue_step_io(thallama_decoder* d, const StepIO& io) {
     p.rms_w = w.rms_final_weight;
     p.xn = d->xn_d;
     if (d->L > 0) norm_from_ssq(d, p);
-    if (d->L == 0) {
+    if (d->L == 0 && io.embed) {
       p.tok = io.tok;
       p.emb = w.token_embedding_table;
       p.x_out = io.x;
@@ -1280,25 +1319,250 @@ extern "C" thablasStatus_t thaDNN_s_forward_batch(thablasHandle_t handle1, thabl
   return THABLAS_STATUS_SUCCESS;
 }
 
-// Out of scope: the reference's 70B and pipeline drivers (src/thaDNN.cpp:83-427).
-extern "C" thablasStatus_t thaDNN_s_forward_70B(thablasHandle_t, int, Config*, TransformerWeights*[], RunState*,
-                                               TransformerWeights*, RunState*, int[], int[], float*) {
-  return THABLAS_STATUS_NOT_SUPPORTED;
+// ------------------------------------------------------------------ pipeline stages (§8(f4))
+// The reference's pipeline drivers (src/thaDNN.cpp:191-427) split the layers over devices:
+// device g holds layers [g * pipe, (g + 1) * pipe) (copy_transformer_weight_pipeline_to_device_
+// batch), runs them for the batch, and hands the residual stream x to device g + 1; the last
+// device runs the final norm and the classifier.  Here a stage is a decoder over the stage's
+// layer range (cfg.n_layers = pipe) on the multi-launch step: the first stage embeds the tokens,
+// the others start from x, and the hand-off is an asynchronous peer copy over xGMI on the stage's
+// stream followed by an event the next stage's stream waits on, so no host thread blocks between
+// stages (the reference synchronises the device after every stage).
+//
+// One stage: tokens / positions in, the layers, then (last stage) logits into logits_h and a
+// synchronisation, or (x_next) the residual stream copied into the next stage's x (device
+// next_dev) and this stage's event recorded.  wait: the previous stage's decoder (its event).
+extern "C" int thallama_decoder_stage(thallama_decoder* d, const int* token_h, const int* pos_h, int embed,
+                                      float* logits_h, const thallama_decoder* wait, float* x_next, int next_dev) {
+  if (!d || !token_h || !pos_h) return (int)hipErrorInvalidValue;
+  int r = upload_tok_pos(d, token_h, pos_h);
+  if (r) return r;
+  if (wait) TL_TRY(hipStreamWaitEvent(d->stream, wait->ev_stage, 0));
+  StepIO io = step_io(d);
+  io.embed = embed != 0;
+  io.logits = logits_h ? d->s.logits : nullptr;
+  if ((r = enqueue_step_io(d, io)) != 0) return r;
+  if (logits_h) {
+    TL_TRY(hipMemcpyAsync(logits_h, d->s.logits, sizeof(float) * (size_t)d->B * d->V, hipMemcpyDeviceToHost,
+                          d->stream));
+    TL_TRY(hipStreamSynchronize(d->stream));
+    return 0;
+  }
+  if (x_next) {
+    const size_t bytes = sizeof(float) * (size_t)d->B * d->dim;
+    if (next_dev == d->dev) TL_TRY(hipMemcpyAsync(x_next, d->s.x, bytes, hipMemcpyDeviceToDevice, d->stream));
+    else TL_TRY(hipMemcpyPeerAsync(x_next, next_dev, d->s.x, d->dev, bytes, d->stream));
+  }
+  TL_TRY(hipEventRecord(d->ev_stage, d->stream));
+  return 0;
 }
-extern "C" thablasStatus_t thaDNN_s_forward_batch_pipe_line(thablasHandle_t[], int, int, Transformer*[], int[], int[],
-                                                           float*) {
-  return THABLAS_STATUS_NOT_SUPPORTED;
+
+// thaDNN_s_forward_70B's step on decoder d: d->w's per-layer tensors are staging slot 0 (slot 1
+// follows it, alloc_weight_to_device_70B), h_w[l] the host copies of layer l.
+static int forward_layer_streamed(thallama_decoder* d, TransformerWeights* h_w[], const int* token, const int* pos,
+                                  float* logits_h) {
+  const long long dim = d->dim, kvd = d->kv_dim, hid = d->hidden;
+  const long long slot = 2 * dim + 2 * dim * dim + 2 * dim * kvd + 3 * dim * hid;  // floats per layer
+  if (d->q8 || d->w.rms_ffn_weight != d->w.rms_att_weight + dim) {
+    g_last_error = "thaDNN_s_forward_70B: device weights not from alloc_weight_to_device_70B";
+    return (int)hipErrorInvalidValue;
+  }
+  if (!d->copy_stream) {
+    ApiLock lock(api_mu());
+    TL_TRY(hipStreamCreateWithFlags(&d->copy_stream, hipStreamNonBlocking));
+    for (int i = 0; i < 2; ++i) {
+      TL_TRY(hipEventCreateWithFlags(&d->ev_copied[i], hipEventDisableTiming));
+      TL_TRY(hipEventCreateWithFlags(&d->ev_used[i], hipEventDisableTiming));
+    }
+  }
+  int r = upload_tok_pos(d, token, pos);
+  if (r) return r;
+  auto slot_w = [&](int l) {
+    const long long o = (l & 1) * slot;
+    const TransformerWeights& w = d->w;
+    return LayerW{w.rms_att_weight + o, w.wq + o, w.wk + o, w.wv + o, w.wo + o, w.rms_ffn_weight + o, w.w1 + o,
+                  w.w2 + o, w.w3 + o};
+  };
+  // layer l's nine tensors into slot l & 1, once the layer that used the slot before is done
+  auto copy_layer = [&](int l) -> int {
+    const LayerW dst = slot_w(l);
+    const TransformerWeights* h = h_w[l];
+    if (!h) {
+      g_last_error = "thaDNN_s_forward_70B: missing host layer";
+      return (int)hipErrorInvalidValue;
+    }
+    if (l >= 2) TL_TRY(hipStreamWaitEvent(d->copy_stream, d->ev_used[l & 1], 0));
+    const struct { const float* dst; const float* src; long long n; } t[9] = {
+        {dst.rms_att, h->rms_att_weight, dim}, {dst.rms_ffn, h->rms_ffn_weight, dim}, {dst.wq, h->wq, dim * dim},
+        {dst.wk, h->wk, dim * kvd}, {dst.wv, h->wv, dim * kvd}, {dst.wo, h->wo, dim * dim},
+        {dst.w1, h->w1, dim * hid}, {dst.w2, h->w2, dim * hid}, {dst.w3, h->w3, dim * hid}};
+    for (const auto& e : t)
+      TL_TRY(hipMemcpyAsync(const_cast<float*>(e.dst), e.src, sizeof(float) * e.n, hipMemcpyHostToDevice, d->copy_stream));
+    TL_TRY(hipEventRecord(d->ev_copied[l & 1], d->copy_stream));
+    return 0;
+  };
+  if (d->L > 0 && (r = copy_layer(0)) != 0) return r;
+  StepIO io = step_io(d);
+  io.layer_w = slot_w;
+  io.before_layer = [&](int l) -> int {
+    if (l + 1 < d->L) {
+      const int e = copy_layer(l + 1);  // overlaps layer l
+      if (e) return e;
+    }
+    TL_TRY(hipStreamWaitEvent(d->stream, d->ev_copied[l & 1], 0));
+    return 0;
+  };
+  io.after_layer = [&](int l) -> int {
+    TL_TRY(hipEventRecord(d->ev_used[l & 1], d->stream));
+    return 0;
+  };
+  if ((r = enqueue_step_io(d, io)) != 0) return r;
+  TL_TRY(hipMemcpyAsync(logits_h, d->s.logits, sizeof(float) * (size_t)d->V, hipMemcpyDeviceToHost, d->stream));
+  TL_TRY(hipStreamSynchronize(d->stream));
+  return 0;
 }
-extern "C" thablasStatus_t thaDNN_s_forward_batch_multiple_pipe_line(thablasHandle_t[], int, int, int, int, Config*,
-                                                                    TransformerWeights*[], RunState*[], int[], int[],
-                                                                    float*, int*, int*, THALLAMA_OMP_LOCK*) {
-  return THABLAS_STATUS_NOT_SUPPORTED;
+
+namespace {
+// Peer access between the stages' devices, once per ordered pair (the x hand-off).
+void enable_peer(int from, int to) {
+  static std::mutex mu;
+  static std::vector<std::pair<int, int>> done;
+  std::lock_guard<std::mutex> g(mu);
+  for (auto& e : done)
+    if (e.first == from && e.second == to) return;
+  int can = 0;
+  if (hipDeviceCanAccessPeer(&can, from, to) == hipSuccess && can) {
+    ApiLock lock(api_mu());
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(from);
+    (void)hipDeviceEnablePeerAccess(to, 0);  // (already enabled: fine)
+    (void)hipGetLastError();
+    (void)hipSetDevice(cur);
+  }
+  done.emplace_back(from, to);
 }
-extern "C" thablasStatus_t thaDNN_s_forward_batch_multiple_pipe_line_layer_swap(thablasHandle_t[], int, int, int, int,
-                                                                               int, Config*, TransformerWeights*[],
-                                                                               RunState*[], RunState*[], int[], int[],
-                                                                               float*, THALLAMA_OMP_LOCK*) {
-  return THABLAS_STATUS_NOT_SUPPORTED;
+
+// The pipeline forward over n stages: stage g runs on the device of handle[g]'s stream with the
+// stage's weights w[g] and this caller's state s[g].  Stage decoders are cached like
+// thaDNN_s_forward_batch's (key: the stage's config and stream, a tag bit in the vocab field) and
+// held for the whole call, in stage order.
+int pipeline_forward(thablasHandle_t handle[], int n, int B, const Config* p, TransformerWeights* w[], RunState* s[],
+                     const int* token, const int* pos, float* logits_host, const char* who) {
+  if (!handle || !p || !w || !s || !token || !pos || !logits_host || n <= 0 || B <= 0 || p->n_layers % n)
+    return (int)hipErrorInvalidValue;
+  int dev0 = 0;
+  TL_TRY(hipGetDevice(&dev0));
+  Config c = *p;
+  c.n_layers = p->n_layers / n;
+  const int V = c.vocab_size < 0 ? -c.vocab_size : c.vocab_size;
+  std::vector<int> tk(token, token + B), ps(pos, pos + B), dev((size_t)n);
+  for (int b = 0; b < B; ++b)  // idle slots of the reference's scheduler: token 0 at position 0
+    if (tk[b] < 0 || tk[b] >= V || ps[b] < 0 || ps[b] >= c.seq_len) tk[b] = ps[b] = 0;
+  std::vector<std::shared_ptr<CachedDecoder>> st((size_t)n);
+  std::vector<std::unique_lock<std::mutex>> held;
+  int r = 0;
+  for (int g = 0; g < n && !r; ++g) {
+    if ((r = (int)hipStreamGetDevice(handle[g].calc_stream, &dev[g])) != 0) break;
+    if ((r = (int)hipSetDevice(dev[g])) != 0) break;
+    DecKey key(dev[g], handle[g].calc_stream, B, c.dim, c.hidden_dim, c.n_layers, c.n_heads, c.n_kv_heads, c.seq_len,
+               V | (1 << 30) /* stage keyspace */);
+    {
+      std::lock_guard<std::mutex> lk(g_dec_mu);
+      st[g] = dec_lookup(key, &c, w[g], nullptr, s[g], B, handle[g].calc_stream);
+    }
+    if (!st[g]) {
+      fprintf(stderr, "%s: stage %d: %s\n", who, g, thallama_last_error());
+      r = (int)hipErrorInvalidValue;
+      break;
+    }
+    held.emplace_back(st[g]->use);
+    if (g > 0 && dev[g] != dev[g - 1]) enable_peer(dev[g - 1], dev[g]);
+  }
+  for (int g = 0; g < n && !r; ++g) {
+    if ((r = (int)hipSetDevice(dev[g])) != 0) break;
+    const bool last = g == n - 1;
+    r = thallama_decoder_stage(st[g]->d, tk.data(), ps.data(), g == 0, last ? logits_host : nullptr,
+                               g > 0 ? st[g - 1]->d : nullptr, last ? nullptr : s[g + 1]->x, last ? 0 : dev[g + 1]);
+    if (r) fprintf(stderr, "%s: stage %d: %s\n", who, g, thallama_last_error());
+  }
+  (void)hipSetDevice(dev0);
+  return r;
+}
+
+thablasStatus_t status_of(int r) {
+  return r == 0 ? THABLAS_STATUS_SUCCESS
+                : r == (int)hipErrorInvalidValue ? THABLAS_STATUS_INVALID_VALUE : THABLAS_STATUS_EXECUTION_FAILED;
+}
+}  // namespace
+
+// ------------------------------------------------------------------ layer streaming (§8(f4))
+// reference src/thaDNN.cpp:83-189 (test_70B, src/llama.cpp:1085-1230): a model whose weights do not
+// fit the device keeps each layer in pinned host memory (h_w[l], copy_transformer_to_host_70B) and
+// streams it in per step.  The reference copies a layer, synchronises, computes it, and also moves
+// that layer's K/V rows in and out of host memory every layer.  Here layer l + 1's nine tensors
+// are copied on a second stream into the other of two device staging slots (alloc_weight_to_
+// device_70B) while layer l computes (events: slot copied / slot consumed), and the K/V cache
+// stays on the device (alloc_state_to_device_70B allocates every layer's: an MI355X's 288 GB hold
+// a 70B model's cache with room to spare), so h_s is not used.  Batch 1, like the reference.
+extern "C" thablasStatus_t thaDNN_s_forward_70B(thablasHandle_t handle, int batch_size, Config* p,
+                                               TransformerWeights* h_w[], RunState* h_s, TransformerWeights* d_w,
+                                               RunState* d_s, int token[], int pos[], float* logits_host) {
+  (void)h_s;
+  if (!p || !h_w || !d_w || !d_s || !token || !pos || !logits_host || batch_size != 1) return THABLAS_STATUS_INVALID_VALUE;
+  int dev = 0;
+  CHECK_HIP(hipGetDevice(&dev));
+  const int V = p->vocab_size < 0 ? -p->vocab_size : p->vocab_size;
+  if (token[0] < 0 || token[0] >= V || pos[0] < 0 || pos[0] >= p->seq_len) return THABLAS_STATUS_INVALID_VALUE;
+  DecKey key(dev, handle.calc_stream, 1, p->dim, p->hidden_dim, p->n_layers, p->n_heads, p->n_kv_heads, p->seq_len,
+             V | (1 << 29) /* layer-streaming keyspace */);
+  const int r = with_cached_decoder(key, p, d_w, nullptr, d_s, 1, handle.calc_stream, "thaDNN_s_forward_70B",
+                                    [&](thallama_decoder* d) { return forward_layer_streamed(d, h_w, token, pos, logits_host); });
+  return status_of(r);
+}
+
+// reference src/thaDNN.cpp:191-289.  host_thread_status / device_host_thread / device_mtx are the
+// reference scheduler's bookkeeping: its per-device locks serialise host threads on a device; the
+// stages here run on each caller's own streams and states, so callers may share devices freely.
+extern "C" thablasStatus_t thaDNN_s_forward_batch_multiple_pipe_line(thablasHandle_t handle[], int host_thread_id,
+                                                                    int n_host_threads, int n_devices, int batch_size,
+                                                                    Config* p, TransformerWeights* w[], RunState* s[],
+                                                                    int token[], int pos[], float* logits_host,
+                                                                    int* host_thread_status, int* device_host_thread,
+                                                                    THALLAMA_OMP_LOCK* device_mtx) {
+  (void)host_thread_id; (void)n_host_threads; (void)host_thread_status; (void)device_host_thread; (void)device_mtx;
+  return status_of(pipeline_forward(handle, n_devices, batch_size, p, w, s, token, pos, logits_host,
+                                    "thaDNN_s_forward_batch_multiple_pipe_line"));
+}
+
+// reference src/thaDNN.cpp:291-427: the same pipeline with the K/V rows past n_buffer_words kept in
+// host memory and swapped per layer (its GPUs could not hold the whole cache).  An MI355X holds
+// every position (alloc_swap_run_state_to_device_batch allocates the full cache), so nothing is
+// swapped and s_host_batch is not used.
+extern "C" thablasStatus_t thaDNN_s_forward_batch_multiple_pipe_line_layer_swap(
+    thablasHandle_t handle[], int thread_id, int n_host_threads, int n_devices, int batch_size, int n_buffer_words,
+    Config* p, TransformerWeights* w[], RunState* s[], RunState* s_host_batch[], int token[], int pos[],
+    float* logits_host, THALLAMA_OMP_LOCK* device_locks) {
+  (void)thread_id; (void)n_host_threads; (void)n_buffer_words; (void)s_host_batch; (void)device_locks;
+  return status_of(pipeline_forward(handle, n_devices, batch_size, p, w, s, token, pos, logits_host,
+                                    "thaDNN_s_forward_batch_multiple_pipe_line_layer_swap"));
+}
+
+// reference include/thaDNN.hpp:74 (declared there, never defined): the pipeline over one
+// Transformer per device (weights and state from copy_transformer_pipeline_to_device_batch).
+extern "C" thablasStatus_t thaDNN_s_forward_batch_pipe_line(thablasHandle_t handle[], int n_devices, int n_batches,
+                                                           Transformer* transformer_d[], int token[], int pos[],
+                                                           float* logits_host) {
+  if (!transformer_d || n_devices <= 0) return THABLAS_STATUS_INVALID_VALUE;
+  std::vector<TransformerWeights*> w((size_t)n_devices);
+  std::vector<RunState*> s((size_t)n_devices);
+  for (int g = 0; g < n_devices; ++g) {
+    if (!transformer_d[g]) return THABLAS_STATUS_INVALID_VALUE;
+    w[g] = &transformer_d[g]->weights;
+    s[g] = &transformer_d[g]->state;
+  }
+  return status_of(pipeline_forward(handle, n_devices, n_batches, &transformer_d[0]->config, w.data(), s.data(), token,
+                                    pos, logits_host, "thaDNN_s_forward_batch_pipe_line"));
 }
 
 // ------------------------------------------------------------------ int8 (runq Q8_0) decoder

@@ -229,62 +229,204 @@ extern "C" void alloc_state_to_device_batch(Transformer* t_h, RunState*& s_d_bat
 extern "C" void free_state_device(RunState* s) {
   if (!s) return;
   tl::ApiLock lock(tl::api_mu());
-  float* bufs[] = {s->x, s->xb, s->xb2, s->hb, s->hb2, s->q, s->att, s->logits, s->key_cache, s->value_cache};
+  float* bufs[] = {s->x,         s->xb,          s->xb2,        s->hb,         s->hb2,
+                   s->q,         s->att,         s->logits,     s->key_cache,  s->value_cache,
+                   s->key_matmul, s->value_matmul, s->key_layer_cache, s->value_layer_cache};
   for (float* b : bufs)
     if (b) CHECK_HIP(hipFree(b));
   free(s);
 }
 
-// ------------------------------------------------------------------ out of scope
-// The reference's pipeline, layer-swap and 70B staging (src/models.cpp:181-760; drivers
-// src/thaDNN.cpp:83-427): 7B fits one MI355X's 288 GB, so none is rebuilt.  Declared with the
-// reference signatures so its src/llama.cpp links unchanged; its main() never reaches them.
-static void unsupported(const char* what) {
-  fprintf(stderr, "libthallama: %s is not supported (pipeline / layer-swap / 70B drivers are out of scope: "
-                  "the model fits one MI355X)\n", what);
+// ------------------------------------------------------------------ pipeline / 70B residency (§8(f4))
+// The reference's staging for its pipeline and layer-streaming drivers (src/models.cpp:181-758),
+// with the same signatures and what they hand the drivers (forward.hip: pipeline_forward,
+// thaDNN_s_forward_70B).  Each device's share is ONE arena and the copies are ranges of the
+// mmapped payload; the run states use the decoder's cache layout [batch][layers][seq][kv_dim].
+
+// (layers [pipe_id * pipe_size, +pipe_size) of t_h) -> one device arena: embedding | rms_att |
+// rms_ffn | wq | wk | wv | wo | w1 | w2 | w3 | rms_final | wcls (a shared classifier points at the
+// embedding)
+static TransformerWeights* upload_pipeline_weights(const Transformer* t_h, int pipe_size, int pipe_id) {
+  const Config* p = &t_h->config;
+  const size_t dim = p->dim, hid = p->hidden_dim, V = p->vocab_size < 0 ? -p->vocab_size : p->vocab_size;
+  const size_t kvd = (size_t)p->dim * p->n_kv_heads / p->n_heads, P = pipe_size, l0 = (size_t)pipe_id * pipe_size;
+  const TransformerWeights& h = t_h->weights;
+  const bool shared = h.wcls == h.token_embedding_table;
+  const struct { const float* src; size_t n; } part[12] = {
+      {h.token_embedding_table, V * dim}, {h.rms_att_weight + l0 * dim, P * dim}, {h.rms_ffn_weight + l0 * dim, P * dim},
+      {h.wq + l0 * dim * dim, P * dim * dim}, {h.wk + l0 * dim * kvd, P * dim * kvd}, {h.wv + l0 * dim * kvd, P * dim * kvd},
+      {h.wo + l0 * dim * dim, P * dim * dim}, {h.w1 + l0 * dim * hid, P * dim * hid}, {h.w2 + l0 * dim * hid, P * dim * hid},
+      {h.w3 + l0 * dim * hid, P * dim * hid}, {h.rms_final_weight, dim}, {h.wcls, shared ? 0 : V * dim}};
+  size_t total = 0;
+  for (const auto& e : part) total += e.n;
+  float* arena = nullptr;
+  tl::ApiLock lock(tl::api_mu());
+  CHECK_HIP(hipMalloc(&arena, total * sizeof(float)));
+  float* dst[12];
+  size_t off = 0;
+  for (int i = 0; i < 12; ++i) {
+    dst[i] = arena + off;
+    if (part[i].n) CHECK_HIP(hipMemcpy(dst[i], part[i].src, part[i].n * sizeof(float), hipMemcpyHostToDevice));
+    off += part[i].n;
+  }
+  TransformerWeights* w = (TransformerWeights*)calloc(1, sizeof(TransformerWeights));
+  w->token_embedding_table = dst[0];
+  w->rms_att_weight = dst[1]; w->rms_ffn_weight = dst[2];
+  w->wq = dst[3]; w->wk = dst[4]; w->wv = dst[5]; w->wo = dst[6]; w->w1 = dst[7]; w->w2 = dst[8]; w->w3 = dst[9];
+  w->rms_final_weight = dst[10];
+  w->wcls = shared ? dst[0] : dst[11];
+  return w;
 }
+
+// A run state for `batch` sequences over `layers` layers (the decoder's layout); key/value_matmul
+// are the reference pipeline's per-step K/V rows (kept for the struct's users; the decoder writes
+// K/V straight into the cache).
+static RunState* alloc_stage_state(const Config* p, int layers, int batch) {
+  const size_t dim = p->dim, V = p->vocab_size < 0 ? -p->vocab_size : p->vocab_size, H = p->n_heads, S = p->seq_len;
+  const size_t hid = p->hidden_dim, kvd = (size_t)p->dim * p->n_kv_heads / p->n_heads, B = batch, L = layers;
+  RunState* s = (RunState*)calloc(1, sizeof(RunState));
+  tl::ApiLock lock(tl::api_mu());
+  CHECK_HIP(hipMalloc(&s->x, dim * B * 4));
+  CHECK_HIP(hipMalloc(&s->xb, dim * B * 4));
+  CHECK_HIP(hipMalloc(&s->xb2, dim * B * 4));
+  CHECK_HIP(hipMalloc(&s->hb, hid * B * 4));
+  CHECK_HIP(hipMalloc(&s->hb2, hid * B * 4));
+  CHECK_HIP(hipMalloc(&s->q, dim * B * 4));
+  CHECK_HIP(hipMalloc(&s->att, H * S * B * 4));
+  CHECK_HIP(hipMalloc(&s->logits, V * B * 4));
+  CHECK_HIP(hipMalloc(&s->key_cache, L * S * kvd * B * 4));
+  CHECK_HIP(hipMalloc(&s->value_cache, L * S * kvd * B * 4));
+  CHECK_HIP(hipMemset(s->key_cache, 0, L * S * kvd * B * 4));
+  CHECK_HIP(hipMemset(s->value_cache, 0, L * S * kvd * B * 4));
+  CHECK_HIP(hipMalloc(&s->key_matmul, kvd * B * 4));
+  CHECK_HIP(hipMalloc(&s->value_matmul, kvd * B * 4));
+  return s;
+}
+
 extern "C" void set_transformer(void) {}
-extern "C" void copy_transformer_pipeline_to_device(thablasHandle_t, Transformer*, Transformer*& t_d, int, int) {
-  unsupported(__func__);
-  t_d = nullptr;
+
+// reference src/models.cpp:327-372
+extern "C" void copy_transformer_weight_pipeline_to_device_batch(Transformer* t_h, TransformerWeights*& w_d, int pipe_size,
+                                                                 int pipe_id, int batch_size) {
+  (void)batch_size;
+  w_d = upload_pipeline_weights(t_h, pipe_size, pipe_id);
 }
-extern "C" void copy_transformer_pipeline_to_device_batch(thablasHandle_t, Transformer*, Transformer*& t_d, int, int,
-                                                          int) {
-  unsupported(__func__);
-  t_d = nullptr;
+
+// reference src/models.cpp:374-408
+extern "C" void alloc_run_state_to_device_batch(thablasHandle_t, Transformer* t_h, RunState*& s_d, int pipe_size, int pipe_id,
+                                                int batch_size) {
+  (void)pipe_id;
+  s_d = alloc_stage_state(&t_h->config, pipe_size, batch_size);
 }
-extern "C" void copy_transformer_weight_pipeline_to_device_batch(Transformer*, TransformerWeights*& w_d, int, int, int) {
-  unsupported(__func__);
-  w_d = nullptr;
+
+// reference src/models.cpp:255-325: weights and state of one stage in a device Transformer (its
+// config stays the whole model's)
+extern "C" void copy_transformer_pipeline_to_device_batch(thablasHandle_t, Transformer* t_h, Transformer*& t_d, int pipe_size,
+                                                          int pipe_id, int batch_size) {
+  t_d = (Transformer*)calloc(1, sizeof(Transformer));
+  t_d->config = t_h->config;
+  TransformerWeights* w = upload_pipeline_weights(t_h, pipe_size, pipe_id);
+  t_d->weights = *w;
+  free(w);
+  RunState* s = alloc_stage_state(&t_h->config, pipe_size, batch_size);
+  t_d->state = *s;
+  free(s);
+  t_d->fd = -1;
 }
-extern "C" void alloc_run_state_to_device_batch(thablasHandle_t, Transformer*, RunState*& s_d, int, int, int) {
-  unsupported(__func__);
-  s_d = nullptr;
+
+// reference src/models.cpp:181-253
+extern "C" void copy_transformer_pipeline_to_device(thablasHandle_t handle, Transformer* t_h, Transformer*& t_d, int pipe_size,
+                                                    int pipe_id) {
+  copy_transformer_pipeline_to_device_batch(handle, t_h, t_d, pipe_size, pipe_id, 1);
 }
+
+// reference src/models.cpp:410-440: the host half of the layer-swapped cache.  An MI355X keeps the
+// whole cache on the device (below), so the host state holds no buffers.
 extern "C" void alloc_swap_run_state_on_host_batch(thablasHandle_t, Transformer*, RunState*& s_h, int, int, int, int) {
-  unsupported(__func__);
-  s_h = nullptr;
+  s_h = (RunState*)calloc(1, sizeof(RunState));
 }
-extern "C" void alloc_swap_run_state_to_device_batch(thablasHandle_t, Transformer*, RunState*& s_d, int, int, int,
-                                                     int) {
-  unsupported(__func__);
-  s_d = nullptr;
+
+// reference src/models.cpp:442-476: the device half, n_buffer_words positions there and the rest
+// swapped to host per layer; here every position (seq_len) lives on the device.
+extern "C" void alloc_swap_run_state_to_device_batch(thablasHandle_t, Transformer* t_h, RunState*& s_d, int pipe_size, int,
+                                                     int batch_size, int n_buffer_words) {
+  (void)n_buffer_words;
+  s_d = alloc_stage_state(&t_h->config, pipe_size, batch_size);
 }
-extern "C" void copy_transformer_to_host_70B(Transformer*, TransformerWeights* h_w[], RunState* h_s[], int n_devices) {
-  unsupported(__func__);
-  for (int i = 0; i < n_devices; ++i) {
-    if (h_w) h_w[i] = nullptr;
-    if (h_s) h_s[i] = nullptr;
+
+// reference src/models.cpp:511-692: every layer's weights in pinned host memory (H2D copies at the
+// link's full rate), h_w[l] per layer.  The K/V cache stays on the device (alloc_state_to_device_
+// 70B), so the per-device host states hold no buffers.
+extern "C" void copy_transformer_to_host_70B(Transformer* storage_t, TransformerWeights* h_w[], RunState* h_s[], int n_devices) {
+  const Config* p = &storage_t->config;
+  const size_t dim = p->dim, hid = p->hidden_dim, kvd = (size_t)p->dim * p->n_kv_heads / p->n_heads;
+  const TransformerWeights& s = storage_t->weights;
+  const size_t layer = 2 * dim + 2 * dim * dim + 2 * dim * kvd + 3 * dim * hid;
+  for (int l = 0; l < p->n_layers; ++l) {
+    float* h = nullptr;
+    {
+      tl::ApiLock lock(tl::api_mu());
+      CHECK_HIP(hipHostMalloc(&h, layer * sizeof(float), hipHostMallocDefault));
+    }
+    const size_t L = l;
+    TransformerWeights* w = (TransformerWeights*)calloc(1, sizeof(TransformerWeights));
+    const struct { float** dst; const float* src; size_t n; } t[9] = {
+        {&w->rms_att_weight, s.rms_att_weight + L * dim, dim}, {&w->rms_ffn_weight, s.rms_ffn_weight + L * dim, dim},
+        {&w->wq, s.wq + L * dim * dim, dim * dim}, {&w->wk, s.wk + L * dim * kvd, dim * kvd},
+        {&w->wv, s.wv + L * dim * kvd, dim * kvd}, {&w->wo, s.wo + L * dim * dim, dim * dim},
+        {&w->w1, s.w1 + L * dim * hid, dim * hid}, {&w->w2, s.w2 + L * dim * hid, dim * hid},
+        {&w->w3, s.w3 + L * dim * hid, dim * hid}};
+    for (const auto& e : t) {
+      *e.dst = h;
+      memcpy(h, e.src, e.n * sizeof(float));
+      h += e.n;
+    }
+    h_w[l] = w;
+  }
+  for (int g = 0; g < n_devices; ++g) h_s[g] = (RunState*)calloc(1, sizeof(RunState));
+}
+
+// reference src/models.cpp:694-717: one sequence's state; every layer's K/V rows live here
+extern "C" void alloc_state_to_device_70B(Transformer* t_h, RunState*& d_s) {
+  d_s = alloc_stage_state(&t_h->config, t_h->config.n_layers, 1);
+}
+
+// reference src/models.cpp:719-758: embedding, final norm and classifier on the device, plus two
+// staging slots for the streamed layers (rms_att | rms_ffn | wq | wk | wv | wo | w1 | w2 | w3 each,
+// slot 1 right after slot 0; the per-layer fields point at slot 0)
+extern "C" void alloc_weight_to_device_70B(Transformer* h_t, TransformerWeights*& d_w) {
+  const Config* p = &h_t->config;
+  const size_t dim = p->dim, hid = p->hidden_dim, V = p->vocab_size < 0 ? -p->vocab_size : p->vocab_size;
+  const size_t kvd = (size_t)p->dim * p->n_kv_heads / p->n_heads;
+  const size_t layer = 2 * dim + 2 * dim * dim + 2 * dim * kvd + 3 * dim * hid;
+  const TransformerWeights& h = h_t->weights;
+  const bool shared = h.wcls == h.token_embedding_table;
+  float* a = nullptr;
+  tl::ApiLock lock(tl::api_mu());
+  CHECK_HIP(hipMalloc(&a, (V * dim + dim + (shared ? 0 : V * dim) + 2 * layer) * sizeof(float)));
+  d_w = (TransformerWeights*)calloc(1, sizeof(TransformerWeights));
+  d_w->token_embedding_table = a;
+  CHECK_HIP(hipMemcpy(a, h.token_embedding_table, V * dim * sizeof(float), hipMemcpyHostToDevice));
+  a += V * dim;
+  d_w->rms_final_weight = a;
+  CHECK_HIP(hipMemcpy(a, h.rms_final_weight, dim * sizeof(float), hipMemcpyHostToDevice));
+  a += dim;
+  if (shared) {
+    d_w->wcls = d_w->token_embedding_table;
+  } else {
+    d_w->wcls = a;
+    CHECK_HIP(hipMemcpy(a, h.wcls, V * dim * sizeof(float), hipMemcpyHostToDevice));
+    a += V * dim;
+  }
+  float** f[9] = {&d_w->rms_att_weight, &d_w->rms_ffn_weight, &d_w->wq, &d_w->wk, &d_w->wv, &d_w->wo, &d_w->w1,
+                  &d_w->w2, &d_w->w3};
+  const size_t n[9] = {dim, dim, dim * dim, dim * kvd, dim * kvd, dim * dim, dim * hid, dim * hid, dim * hid};
+  for (int i = 0; i < 9; ++i) {
+    *f[i] = a;
+    a += n[i];
   }
 }
-extern "C" void alloc_state_to_device_70B(Transformer*, RunState*& d_s) {
-  unsupported(__func__);
-  d_s = nullptr;
-}
-extern "C" void alloc_weight_to_device_70B(Transformer*, TransformerWeights*& d_w) {
-  unsupported(__func__);
-  d_w = nullptr;
-}
+
 extern "C" void free_transformer_device(void) {}
 
 // ------------------------------------------------------------------ synthetic weights

@@ -166,6 +166,33 @@ def lib():
             "thallama_decoder_prof": (I, [VP, I, C.POINTER(C.c_double), C.POINTER(C.c_longlong)]),
             "thallama_decoder_prof_reset": (None, [VP]),
             "thallama_step_bytes": (C.c_double, [C.POINTER(Config), I, I, c_int_p]),
+            "thallama_decoder_stage": (I, [VP, c_int_p, c_int_p, I, P, VP, P, I]),
+            "thaDNN_s_forward_70B": (I, [Handle, I, C.POINTER(Config), C.POINTER(C.POINTER(TransformerWeights)),
+                                         C.POINTER(RunState), C.POINTER(TransformerWeights), C.POINTER(RunState),
+                                         c_int_p, c_int_p, P]),
+            "thaDNN_s_forward_batch_pipe_line": (I, [C.POINTER(Handle), I, I, C.POINTER(C.POINTER(Transformer)),
+                                                     c_int_p, c_int_p, P]),
+            "thaDNN_s_forward_batch_multiple_pipe_line": (
+                I, [C.POINTER(Handle), I, I, I, I, C.POINTER(Config), C.POINTER(C.POINTER(TransformerWeights)),
+                    C.POINTER(C.POINTER(RunState)), c_int_p, c_int_p, P, c_int_p, c_int_p, VP]),
+            "thaDNN_s_forward_batch_multiple_pipe_line_layer_swap": (
+                I, [C.POINTER(Handle), I, I, I, I, I, C.POINTER(Config), C.POINTER(C.POINTER(TransformerWeights)),
+                    C.POINTER(C.POINTER(RunState)), C.POINTER(C.POINTER(RunState)), c_int_p, c_int_p, P, VP]),
+            "copy_transformer_weight_pipeline_to_device_batch": (
+                None, [C.POINTER(Transformer), C.POINTER(C.POINTER(TransformerWeights)), I, I, I]),
+            "alloc_run_state_to_device_batch": (None, [Handle, C.POINTER(Transformer), C.POINTER(C.POINTER(RunState)),
+                                                       I, I, I]),
+            "copy_transformer_pipeline_to_device_batch": (
+                None, [Handle, C.POINTER(Transformer), C.POINTER(C.POINTER(Transformer)), I, I, I]),
+            "alloc_swap_run_state_on_host_batch": (None, [Handle, C.POINTER(Transformer), C.POINTER(C.POINTER(RunState)),
+                                                          I, I, I, I]),
+            "alloc_swap_run_state_to_device_batch": (None, [Handle, C.POINTER(Transformer),
+                                                            C.POINTER(C.POINTER(RunState)), I, I, I, I]),
+            "copy_transformer_to_host_70B": (None, [C.POINTER(Transformer), C.POINTER(C.POINTER(TransformerWeights)),
+                                                    C.POINTER(C.POINTER(RunState)), I]),
+            "alloc_state_to_device_70B": (None, [C.POINTER(Transformer), C.POINTER(C.POINTER(RunState))]),
+            "alloc_weight_to_device_70B": (None, [C.POINTER(Transformer), C.POINTER(C.POINTER(TransformerWeights))]),
+            "free_weight_device": (None, [C.POINTER(TransformerWeights)]),
             "thallama_forward_batch_cache_size": (I, []),
             "thallama_forward_batch_live": (I, []),
             "thallama_forward_batch_cache_clear": (None, []),

@@ -105,10 +105,13 @@ void alloc_state_to_device_batch(Transformer* t_h, THALLAMA_OUT(RunState) s_d_ba
 void free_weight_device(TransformerWeights* w_d);
 void free_state_device(RunState* s_d);
 
-// ---- out of scope (7B fits one MI355X's 288 GB): the reference's pipeline,
-// layer-swap and 70B host/device staging (include/models.hpp:120, 125-134).  Declared with the
-// reference signatures so its src/llama.cpp links unchanged; they are never reached from its
-// main().  Each prints that it is unsupported and leaves every out-parameter NULL.
+// ---- pipeline, layer-swap and 70B staging (reference include/models.hpp:120,
+// 125-134, src/models.cpp:181-758) for the drivers in thaDNN.hpp.  A stage's weights are one device
+// arena (free with free_weight_device), its state the decoder's layout [batch][layers][seq][kv_dim]
+// (free_state_device).  The swap variants keep EVERY position on the device (an MI355X holds the
+// cache; the host state is an empty struct), and the 70B device state holds every layer's K/V
+// rows; the 70B device weights hold the embedding, final norm, classifier and two layer staging
+// slots (the per-layer fields point at slot 0).
 void set_transformer(void);
 void copy_transformer_pipeline_to_device(thablasHandle_t handle, Transformer* t_h, THALLAMA_OUT(Transformer) t_d, int pipe_size, int pipe_id);
 void copy_transformer_pipeline_to_device_batch(thablasHandle_t handle, Transformer* t_h, THALLAMA_OUT(Transformer) t_d, int pipe_size, int pipe_id, int batch_size);

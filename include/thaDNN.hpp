@@ -50,10 +50,17 @@ thablasStatus_t thaDNN_s_forward_batch(thablasHandle_t handle1, thablasHandle_t 
                                        TransformerWeights* w, RunState* s_batch, int token[],
                                        int pos[], float* logits_host);
 
-// ---- out of scope (7B fits one MI355X): the 70B layer-streaming and the
-// pipeline / layer-swap drivers (reference include/thaDNN.hpp:72-80, src/thaDNN.cpp:83-427),
-// declared with the reference signatures so its src/llama.cpp links unchanged (they are not
-// reached from its main()).  Each returns THABLAS_STATUS_NOT_SUPPORTED.
+// ---- the 70B layer-streaming and the pipeline / layer-swap drivers (reference
+// include/thaDNN.hpp:72-80, src/thaDNN.cpp:83-427), on the decoder's kernels:
+//  * thaDNN_s_forward_70B: batch 1; layer l + 1's weights (h_w, pinned host memory from
+//    copy_transformer_to_host_70B) copied into a device staging slot while layer l computes;
+//    every layer's K/V rows stay in d_s (h_s unused);
+//  * the pipelines: stage g = layers [g*pipe, (g+1)*pipe) on the device of handle[g]'s stream with
+//    w[g] / s_batch[g] (models.hpp staging), the residual stream handed to the next stage by an
+//    asynchronous peer copy + event, logits from the last stage into logits_host (synchronised).
+//    The reference's host-thread bookkeeping and device locks are accepted and not needed (each
+//    caller runs on its own streams and states); the layer-swap variant swaps nothing (the device
+//    holds every position).  n_layers must be a multiple of n_devices.
 thablasStatus_t thaDNN_s_forward_70B(thablasHandle_t handle, int batch_size, Config* p, TransformerWeights* h_w[], RunState* h_s, TransformerWeights* d_w, RunState* d_s, int token[], int pos[], float* logits_host);
 thablasStatus_t thaDNN_s_forward_batch_pipe_line(thablasHandle_t handle[], int n_devices, int n_batches, Transformer* transformer_d[], int token[], int pos[], float* logits_host);
 thablasStatus_t thaDNN_s_forward_batch_multiple_pipe_line(thablasHandle_t handle[], int host_thread_id, int n_host_threads, int n_devices, int batch_size, Config* p, TransformerWeights* w[], RunState* s_batch[], int token[], int pos[], float* logits_host, int* host_thread_status, int* device_host_thread, THALLAMA_OMP_LOCK* device_mtx);

@@ -125,6 +125,15 @@ int thallama_decoder_sync(thallama_decoder* d);
 int thallama_decoder_prof(thallama_decoder* d, int kclass, double* total_ms, long long* count);
 void thallama_decoder_prof_reset(thallama_decoder* d);
 
+/* One pipeline stage (thaDNN_s_forward_batch_multiple_pipe_line's building block): decoder d is
+ * built over the stage's layer range (cfg.n_layers = layers of the stage).  embed: layer 0 reads
+ * the tokens' embedding rows (first stage), else d's RunState x holds the input.  logits_h
+ * (last stage): final norm + classifier, logits copied out, synchronised.  Otherwise x_next
+ * (device next_dev) receives the residual stream and the stage's event is recorded; a later
+ * stage passes this decoder as `wait`.  Multi-launch step, fp32 weights. */
+int thallama_decoder_stage(thallama_decoder* d, const int* token_h, const int* pos_h, int embed, float* logits_h,
+                           const thallama_decoder* wait, float* x_next, int next_dev);
+
 /* thaDNN_s_forward_batch / thaDNN_q8_forward_batch keep one decoder per (device, stream, batch,
  * config, dtype), made for the caller's weight and state buffers; a call with other buffers
  * replaces it, and at most 8 stay cached (least recently used dropped).  Concurrent callers are
