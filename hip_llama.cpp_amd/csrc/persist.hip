@@ -1017,8 +1017,10 @@ bool persistent_prepare(PStep& p, int ncu, const char** why) {
     const unsigned long long bit = dev < 64 ? 1ull << dev : 0ull;
     if (!bit || !(done & bit)) {
       for (const void* f : {kfn<128, false>(), kfn<64, false>(), kfn<128, true>(), kfn<64, true>()})
-        if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+        if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDynLdsCap) != hipSuccess) {
+          (void)hipGetLastError();  // (not sticky for the caller's next launch check)
           return fail("cannot raise the dynamic LDS limit");
+        }
       done |= bit;
     }
   }

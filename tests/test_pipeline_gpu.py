@@ -52,20 +52,20 @@ def test_pipeline_matches_oracle(gpu, oracle, n_stages, variant):
     sps = (C.POINTER(tl.RunState) * n_stages)()
     hsp = (C.POINTER(tl.RunState) * n_stages)()
     tps = (C.POINTER(tl.Transformer) * n_stages)()
-    for g in range(n_stages):
+    for g in range(n_stages):  # (each out-parameter is the reference's `T* &`: a pointer to the pointer)
         if variant == "pipe_line":
-            L.copy_transformer_pipeline_to_device_batch(hs[g], C.byref(t_h), C.byref(tps, g * C.sizeof(tps._type_)),
-                                                        pipe, g, B)
+            tp = C.POINTER(tl.Transformer)()
+            L.copy_transformer_pipeline_to_device_batch(hs[g], C.byref(t_h), C.byref(tp), pipe, g, B)
+            tps[g] = tp
+            continue
+        wp, sp, hp = C.POINTER(tl.TransformerWeights)(), C.POINTER(tl.RunState)(), C.POINTER(tl.RunState)()
+        L.copy_transformer_weight_pipeline_to_device_batch(C.byref(t_h), C.byref(wp), pipe, g, B)
+        if variant == "layer_swap":
+            L.alloc_swap_run_state_on_host_batch(hs[g], C.byref(t_h), C.byref(hp), pipe, g, B, cfg[6] // 2)
+            L.alloc_swap_run_state_to_device_batch(hs[g], C.byref(t_h), C.byref(sp), pipe, g, B, cfg[6] // 2)
         else:
-            L.copy_transformer_weight_pipeline_to_device_batch(C.byref(t_h), C.byref(wps, g * C.sizeof(wps._type_)),
-                                                               pipe, g, B)
-            if variant == "layer_swap":
-                L.alloc_swap_run_state_on_host_batch(hs[g], C.byref(t_h), C.byref(hsp, g * C.sizeof(hsp._type_)),
-                                                     pipe, g, B, cfg[6] // 2)
-                L.alloc_swap_run_state_to_device_batch(hs[g], C.byref(t_h), C.byref(sps, g * C.sizeof(sps._type_)),
-                                                       pipe, g, B, cfg[6] // 2)
-            else:
-                L.alloc_run_state_to_device_batch(hs[g], C.byref(t_h), C.byref(sps, g * C.sizeof(sps._type_)), pipe, g, B)
+            L.alloc_run_state_to_device_batch(hs[g], C.byref(t_h), C.byref(sp), pipe, g, B)
+        wps[g], sps[g], hsp[g] = wp, sp, hp
     rng = np.random.default_rng(7 + n_stages)
     refs = [oracle.Model(cfg, shared, seed=seed) for _ in range(B)]
     toks = rng.integers(0, cfg[5], (steps + 5, B))
