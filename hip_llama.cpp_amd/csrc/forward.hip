@@ -374,6 +374,11 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
   d->nt = wbytes > 1024.0 * 1024.0 * 1024.0;
   // persistent step: batch 1, fp32 (decided again for int8 in _create_q8)
   TL_TRY(hipDeviceGetAttribute(&d->ncu, hipDeviceAttributeMultiprocessorCount, d->dev));
+  {  // THALLAMA_PERSIST_GRID=n: the persistent step on n blocks (< one per CU; measurements)
+    const char* e = getenv("THALLAMA_PERSIST_GRID");
+    const int n = e ? atoi(e) : 0;
+    if (n >= 8 && n < d->ncu) d->ncu = n;
+  }
   {
     tl::PStep ps = {};
     ps.dim = d->dim; ps.hid = d->hidden; ps.kvd = d->kv_dim; ps.hs = d->hs; ps.NS = d->nsplit;
