@@ -640,16 +640,13 @@ TL_DEVICE void attn_unit_split(const AttnWaveParams& w, int h, int c, int NG, fl
 // fp32 persistent step (batch 1): attn_unit with the keys in LDS windows.  attn_unit holds one
 // 16-key chunk in registers per memory latency, so at long contexts a unit's key range (T / NS
 // keys) is a chain of latencies (7B at position 2000: ~15 chunks, ~30 us per layer).  Here the
-// unit's keys come in rounds of up to 64: K rows transposed (piece i of key l at kw[i * 256 + 4 l])
-// and V rows (vw[u * HS + c]) by LDS-DMA, all of a round requested at once — one latency per 64
-// keys; one lane per key for the scores, online softmax across rounds, a lane's VPL columns for
+// unit's keys come in rounds of up to 64: K rows row-major (key l at kw[l * HS], read by its lane
+// from piece l on: conflict-free) and V rows (vw[u * HS + c]) by LDS-DMA, all of a round requested
+// at once — one latency per 64 keys; one lane per key for the scores, online softmax across rounds, a lane's VPL columns for
 // the output.  Unit s of (b, h) takes the contiguous keys [T s / nact, T (s+1) / nact); the last
 // row (T-1, written by this launch's QKV phase) comes from the granules.  Partials combine as in
 // attn_unit (same records and tickets).  win: attn_win_floats(HS) floats of LDS.
 __host__ __device__ constexpr int attn_win_floats(int hs) { return 2 * 64 * hs + 2 * hs; }
-#ifndef ATTN_K_TRANSPOSED
-#define ATTN_K_TRANSPOSED 0
-#endif
 
 template <int HS>
 TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int lane) {
@@ -678,18 +675,12 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
   // t0 into slots nothing reads), so the waits below can count them: the next round's K rows land
   // while this round's V rows are folded, its V rows while its scores are taken (K and V share no
   // LDS, one window of each).  A single-round unit (short contexts) issues only its n rows.
-  // K rows whole, RPI per wave-instruction (coalesced 1-KiB pieces; a transposed image would
-  // gather 64 rows x 16 B per instruction); the lane-per-key dot below walks its row from piece
-  // `lane` on, so the 16 lanes of a read hit 16 different bank groups
+  // K rows whole, RPI per wave-instruction (coalesced 1-KiB pieces; a transposed image, one 16-B
+  // piece of 64 rows per instruction, measured the same on one box: profiles/r04/attn_k_layout_
+  // ab.json); the lane-per-key dot below walks its row from piece `lane` on, so the 16 lanes of a
+  // read hit 16 different bank groups
   const bool multi = ke - k0 > 64;
   auto issue_k = [&](int t0, int n) {
-#if ATTN_K_TRANSPOSED  // (A/B: the transposed image, one 16-B piece of 64 rows per instruction)
-    const float* row = kbase + (long long)(t0 + (lane < n ? lane : 0)) * p.kv_dim;
-#pragma unroll 4
-    for (int i = 0; i < PC; ++i)
-      if (multi || lane < n) dma16(row + 4 * i, kw + i * 256);
-    return;
-#endif
     const int kq = lane / PC, pc = lane % PC;
     const int ni = multi ? 64 / RPI : (n + RPI - 1) / RPI;
 #pragma unroll 4
@@ -780,9 +771,6 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
     if (multi) wait_all_but_round_half();  // this round's K rows (its V rows may still be in flight)
     else dma_wait_all();
     float sc;
-#if ATTN_K_TRANSPOSED
-    sc = dot(kw + 4 * lane, 64);
-#else
     {  // key `lane`, pieces in the order lane, lane + 1, ... (mod PC)
       float a[4] = {0.f, 0.f, 0.f, 0.f};
       const f4* kr = reinterpret_cast<const f4*>(kw + HS * lane);
@@ -793,7 +781,6 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
       }
       sc = (a[0] + a[1]) + (a[2] + a[3]);
     }
-#endif
     wave_lds_fence();  // the K window's reads are done before the next round lands in it
     if (more) {
       issue_k(t0 + 64, min(64, ke - t0 - 64));

@@ -374,11 +374,6 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
   d->nt = wbytes > 1024.0 * 1024.0 * 1024.0;
   // persistent step: batch 1, fp32 (decided again for int8 in _create_q8)
   TL_TRY(hipDeviceGetAttribute(&d->ncu, hipDeviceAttributeMultiprocessorCount, d->dev));
-  {  // THALLAMA_PERSIST_GRID=n: the persistent step on n blocks (< one per CU; measurements)
-    const char* e = getenv("THALLAMA_PERSIST_GRID");
-    const int n = e ? atoi(e) : 0;
-    if (n >= 8 && n < d->ncu) d->ncu = n;
-  }
   {
     tl::PStep ps = {};
     ps.dim = d->dim; ps.hid = d->hidden; ps.kvd = d->kv_dim; ps.hs = d->hs; ps.NS = d->nsplit;
@@ -791,17 +786,6 @@ static int enqueue_step(thallama_decoder* d) { return enqueue_step_io(d, step_io
 
 static bool use_persist(const thallama_decoder* d) { return d->persist && d->pok; }
 
-// Weight slots per streaming wave the batch-1 persistent step prefetches into L2 / the Infinity
-// Cache while a phase's input is staged (persist.hip prefetch_slots); THALLAMA_PERSIST_PF=n.
-static int persist_pf_slots(bool q8) {
-  static const int v = [] {
-    const char* e = getenv("THALLAMA_PERSIST_PF");
-    return e ? atoi(e) : -1;
-  }();
-  if (v >= 0) return v > 16 ? 16 : v;
-  return q8 ? 0 : 0;
-}
-
 // The whole step (and, for greedy decoding, the argmax + advance) as one persistent launch.
 static int enqueue_persistent(thallama_decoder* d, bool argmax) {
   const TransformerWeights& w = d->w;
@@ -826,7 +810,6 @@ static int enqueue_persistent(thallama_decoder* d, bool argmax) {
   p.argmax = argmax ? 1 : 0;
   p.trace = d->ptrace;
   p.fault = d->pfault ? 1 : 0;
-  p.pf_slots = d->B == 1 ? persist_pf_slots(d->q8) : 0;
   d->pfault = false;  // one-shot (a captured graph keeps it; the give-up drops the graph)
   if (d->q8) {
     p.q8 = d->w8.group_size;

@@ -344,46 +344,6 @@ TL_DEVICE void consume_slot_q8(const PGeo& g, int K, int slot, int lane, const f
   }
 }
 
-// Weight prefetch into L2 / the Infinity Cache while the phase's input is staged (HBM is
-// otherwise idle there): the streaming wave issues default-policy LDS-DMA loads of p.pf_slots of
-// this block's slots past the register-prefetched ones (NBUF * NSW + sw, + NSW, ...) into a
-// 1-KiB LDS strip nobody reads (`dummy`, its own __shared__ object, so the compiler's LDS-DMA
-// alias tracking adds no wait to the staging's LDS accesses).  Issued behind the wave's granule
-// loads, so the gather is not delayed; whichever wave takes such a slot later (take_slot) reads it
-// from the cache.  The data are never consumed from LDS; the waves drain before the kernel ends.
-TL_DEVICE void pf_dma(const void* src, float* dummy) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)dummy, 16, 0, 0);
-}
-
-template <bool Q8>
-TL_DEVICE void prefetch_slots(const PDesc& d, const PGeo& g, const PStep& p, int sw, int lane, float* dummy) {
-  for (int j = 0; j < p.pf_slots; ++j) {
-    const int slot = NBUF * NSW + sw + j * NSW;
-    if (slot >= g.nslot) break;
-    if constexpr (Q8) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int Q = 2 * slot + h;
-        if (Q >= g.nres) break;
-        const int rl = Q / g.nch, c = Q - rl * g.nch;
-        const signed char* row = q8_row_ptr(d, p, g.i0 * d.rpi + rl).q + c * 4096;
-        const int left = g.rowb - c * 4096;
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (u * 1024 + lane * 16 < left) pf_dma(row + u * 1024 + lane * 16, dummy);
-      }
-    } else {
-      const int rl = slot / g.nch, c = slot - rl * g.nch;
-      const char* row = reinterpret_cast<const char*>(row_ptr(d, p, g.i0 * d.rpi + rl)) + c * (PL * 1024);
-      const int left = g.rowb - c * (PL * 1024);
-#pragma unroll
-      for (int u = 0; u < PL; ++u)
-        if (u * 1024 + lane * 16 < left) pf_dma(row + u * 1024 + lane * 16, dummy);
-    }
-  }
-}
-
 // Stream this wave's slots (sw, sw + NSW, ...), sw = streaming-wave index; the NBUF buffers
 // already hold the first NBUF.  Every path loads the buffers in the same places, so the
 // register allocator keeps one set of NBUF register buffers for the whole step.
@@ -812,7 +772,6 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
     }
   } else {
     const int sw = wave - 1;
-    __shared__ __attribute__((aligned(16))) float pf_dummy[256];  // prefetch_slots' write-only strip
     f4 buf[NBUF][PL];
     float sc[NBUF][PL];  // Q8 weight scales (unused for fp32)
     __syncthreads();  // first norm weights preloaded
@@ -840,7 +799,6 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
       auto mid = [&] {
 #pragma unroll
         for (int i = pfn<Q8>(); i < NBUF; ++i) load_any<Q8>(d, g, p, sw + i * NSW, lane, buf[i], sc[i]);
-        if (p.pf_slots) prefetch_slots<Q8>(d, g, p, sw, lane, pf_dummy);
       };
       stage<Q8, false>(d, g, p, xs, xq, xsc, rmsw, red, sqa, wave, lane,
                        tr ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots : nullptr, mid);
@@ -861,7 +819,6 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
       }
       if (tr) TRACE(7);
     }
-    dma_wait_all();  // (prefetches land in LDS: drained before the workgroup can end)
   }
   grid_barrier(p);
   if constexpr (ROLE0) {
@@ -920,8 +877,7 @@ __global__ void __launch_bounds__(PT) persistent_step_kernel(PStep p) {
   else phases<HS, false, Q8>(p, wave, lane, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, etab, tb, awin);
 }
 
-// 160 KiB per CU, less the streaming waves' static 1-KiB prefetch strip (pf_dummy)
-constexpr size_t kDynLdsCap = 160 * 1024 - 1024;
+constexpr size_t kDynLdsCap = 160 * 1024;  // dynamic LDS per block (gfx950: 160 KiB per CU)
 
 static size_t lds_bytes(const PStep& p) {
   return (size_t)(kPResidFloats + kPResFloats + 16 + p.dim + p.pad_floats) * 4 + (size_t)p.q8_pad +

@@ -43,8 +43,6 @@ struct PStep {
   int ang;                  // Q8: attention units per head (persistent_prepare)
   int fault;                // test hook (THALLAMA_OPT_PERSIST_FAULT): block 0 exits at once, as
                             // if the grid were not co-resident; every other wait gives up
-  int pf_slots;             // slots per streaming wave prefetched into L2 / the Infinity Cache by
-                            // LDS-DMA while the phase's input is staged (persist.hip prefetch_slots)
   int B;                    // batched step (persist_b.hip): 2..8 sequences; tok / pos / out and every
                             // hand-off buffer then hold B rows, bmax [grid][8], tickets [L][B*H];
                             // n_scr = the LDS row-chunk partials (persistent_prepare_b)
