@@ -65,6 +65,11 @@ constexpr unsigned kSpinLimit = 1u << 18;
 #ifndef PERSIST_ATTN_WIN
 #define PERSIST_ATTN_WIN 1  // fp32: attention units with their keys in LDS windows (attn_unit_win)
 #endif
+// From this many keys on (fp32, batch 1), the attention phase runs twice as many units (key
+// splits) per head: one on each block's control wave and one on streaming wave 1, whose window is
+// the staging strip (free between the QKV and Wo stagings).  One wave keeps at most ~63 KiB of
+// K/V in flight (vmcnt), so at long contexts the phase is latency-bound per unit.
+constexpr int kAttnHelpMinKeys = 512;
 #ifndef PERSIST_XCD_SKEW
 #define PERSIST_XCD_SKEW 4
 #endif
@@ -744,11 +749,15 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
           for (int u = blockIdx.x; u < p.H * p.ang; u += G)
             attn_unit_split<HS>(aw, u / p.ang, u % p.ang, p.ang, scr, reinterpret_cast<float*>(xs), p.pad_floats, lane);
         } else {
-          const int units = p.H * p.NS;
-          for (int u = blockIdx.x; u < units; u += G) {
+          // long contexts: twice the splits, the second unit of each block on streaming wave 1
+          const bool help = p.attn_help && p.pos[0] + 1 >= kAttnHelpMinKeys;
+          if (help) aw.NS = aw.a.nsplit = 2 * p.NS < kMaxNS ? 2 * p.NS : kMaxNS;
+          const int units = p.H * aw.NS;
+          for (int u = blockIdx.x; u < units; u += (help ? 2 : 1) * G) {
             if constexpr (PERSIST_ATTN_WIN) attn_unit_win<HS>(aw, u, awin, lane);
             else attn_unit<HS, PERSIST_ATTN_CH, true>(aw, u, lane);
           }
+          if (help) __syncthreads();  // the helper's window (the strip) is free for the Wo staging
         }
         TRACE(3);
         continue;
@@ -785,7 +794,29 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
     for (int ph = 0; ph < nph; ++ph) {
       const int l = ph / 5;
       const int kind = ph == nph - 1 ? PK_CLS : ph % 5;
-      if (kind == PK_ATTN) continue;
+      if (kind == PK_ATTN) {
+        if constexpr (!Q8 && PERSIST_ATTN_WIN) {
+          if (p.attn_help && p.pos[0] + 1 >= kAttnHelpMinKeys) {
+            if (sw == 0) {  // the block's second attention unit (control wave: the first)
+              AttnWaveParams aw = {};
+              aw.a.q = p.xb; aw.a.kc = p.kc; aw.a.vc = p.vc;
+              aw.a.kv_b_stride = (long long)p.L * p.S * p.kvd;
+              aw.a.kv_l_off = (long long)l * p.S * p.kvd;
+              aw.a.pos = p.pos; aw.a.out = p.xb; aw.a.part = p.part;
+              aw.a.dim = p.dim; aw.a.kv_dim = p.kvd; aw.a.head_size = HS; aw.a.n_heads = p.H;
+              aw.a.kv_mul = p.kv_mul; aw.a.seq_len = p.S; aw.a.min_chunk = 16;
+              aw.NS = aw.a.nsplit = 2 * p.NS < kMaxNS ? 2 * p.NS : kMaxNS;
+              aw.cnt = p.tickets + (long long)l * p.H; aw.B = 1;
+              aw.gqkv = p.gqkv; aw.gout = p.gxb; aw.etab = etab;
+              aw.tag_in = tb + 5u * l + 1; aw.tag_out = tb + 5u * l + 2; aw.err = p.err;
+              for (int u = blockIdx.x + G; u < p.H * aw.NS; u += 2 * G)
+                attn_unit_win<HS>(aw, u, reinterpret_cast<float*>(xs), lane);
+            }
+            __syncthreads();  // (the control wave's matching barrier ends its attention phase)
+          }
+        }
+        continue;
+      }
       const PDesc d = make_desc<Q8>(p, kind, kind == PK_CLS ? p.L : l, tb);
       const PGeo g = geo<Q8>(d);
       const bool tr = p.trace && sw == 0;
@@ -962,6 +993,13 @@ bool persistent_prepare(PStep& p, int ncu, const char** why) {
     }
   }
   if (lds_bytes(p) > kDynLdsCap) return fail("activations do not fit the LDS");
+  p.attn_help = 0;
+  if (!p.q8 && PERSIST_ATTN_WIN && p.NS * 2 <= kMaxNS) {  // room for a second attention window in the strip?
+    const int base = p.pad_floats, need = attn_win_floats(p.hs);
+    if (base < need) p.pad_floats = need;
+    if (lds_bytes(p) <= kDynLdsCap) p.attn_help = 1;
+    else p.pad_floats = base;
+  }
   {  // allow more than 64 KiB of dynamic LDS (gfx950: 160 KiB per CU): a per-device attribute,
      // raised once for each device a decoder is prepared on (decoders of several devices may be
      // created from several threads, app/run.cpp)

@@ -41,6 +41,8 @@ struct PStep {
                             // attention strip, streaming-wave chain scratch (persistent_prepare)
   int pgp;                  // Q8: row stride (floats) of the long-row products
   int ang;                  // Q8: attention units per head (persistent_prepare)
+  int attn_help;            // fp32 batch 1: the staging strip also holds an attention window, so a
+                            // streaming wave runs a second attention unit per block at long contexts
   int fault;                // test hook (THALLAMA_OPT_PERSIST_FAULT): block 0 exits at once, as
                             // if the grid were not co-resident; every other wait gives up
   int B;                    // batched step (persist_b.hip): 2..8 sequences; tok / pos / out and every
