@@ -170,8 +170,9 @@ struct thallama_decoder {
   bool persist = true;          // requested (THALLAMA_OPT_PERSISTENT)
   bool pfault = false;          // test hook: the next persistent launch loses block 0
   bool pasync = false;          // an asynchronous greedy call ran persistent launches not yet checked
-  hipGraphExec_t exec = nullptr;      // one greedy step (step + argmax), replayed per token
-  hipGraphExec_t exec_fwd = nullptr;  // one forward step (no argmax), replayed by decoder_forward
+  // [lc]: lc = 1 is the persistent step's long-context instantiation (persistent_long_ctx)
+  hipGraphExec_t exec[2] = {};      // one greedy step (step + argmax), replayed per token
+  hipGraphExec_t exec_fwd[2] = {};  // one forward step (no argmax), replayed by decoder_forward
   // persistent one-launch step (persist.hip)
   int ncu = 0;
   unsigned* psync = nullptr;    // [kPSyncWords shards][L*H tickets] (zeroed per launch), err, seq
@@ -202,9 +203,11 @@ struct thallama_decoder {
 // Options, buffers and the persistent path's state are baked into the captured graphs: drop them
 // (recaptured on next use).
 static void drop_graphs(thallama_decoder* d) {
-  if (d->exec) (void)hipGraphExecDestroy(d->exec);
-  if (d->exec_fwd) (void)hipGraphExecDestroy(d->exec_fwd);
-  d->exec = d->exec_fwd = nullptr;
+  for (int i = 0; i < 2; ++i) {
+    if (d->exec[i]) (void)hipGraphExecDestroy(d->exec[i]);
+    if (d->exec_fwd[i]) (void)hipGraphExecDestroy(d->exec_fwd[i]);
+    d->exec[i] = d->exec_fwd[i] = nullptr;
+  }
 }
 
 static int prof_begin(thallama_decoder* d) {
@@ -787,7 +790,13 @@ static int enqueue_step(thallama_decoder* d) { return enqueue_step_io(d, step_io
 static bool use_persist(const thallama_decoder* d) { return d->persist && d->pok; }
 
 // The whole step (and, for greedy decoding, the argmax + advance) as one persistent launch.
-static int enqueue_persistent(thallama_decoder* d, bool argmax) {
+// Which persistent instantiation a step at position pos0 (slot 0, batch 1) runs: 1 = the one with
+// the long-context attention helper (fp32 only; persist.hip).
+static int long_ctx(thallama_decoder* d, int pos0) {
+  return d->B == 1 && !d->q8 && use_persist(d) && tl::persistent_long_ctx(pos0) ? 1 : 0;
+}
+
+static int enqueue_persistent(thallama_decoder* d, bool argmax, int lc) {
   const TransformerWeights& w = d->w;
   const RunState& s = d->s;
   tl::PStep p = {};
@@ -808,6 +817,7 @@ static int enqueue_persistent(thallama_decoder* d, bool argmax) {
   p.sync = d->psync; p.tickets = d->psync + tl::kPSyncWords;
   p.err = d->psync + d->psync_zero; p.seq = p.err + 1; p.bmax = d->pbmax;
   p.argmax = argmax ? 1 : 0;
+  p.long_ctx = lc;
   p.trace = d->ptrace;
   p.fault = d->pfault ? 1 : 0;
   d->pfault = false;  // one-shot (a captured graph keeps it; the give-up drops the graph)
@@ -958,20 +968,21 @@ static int decoder_forward_once(thallama_decoder* d, const int* token_h, const i
   int r = upload_tok_pos(d, token_h, pos_h);
   if (r) return r;
   if (d->use_graph && !d->profile) {  // the step (~160 launches at batch > 1) replayed as one graph
-    if (!d->exec_fwd) {
+    const int lc = long_ctx(d, pos_h[0]);
+    if (!d->exec_fwd[lc]) {
       ApiLock lock(api_mu());
       hipGraph_t g = nullptr;
       TL_TRY(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
-      const int e = use_persist(d) ? enqueue_persistent(d, false) : enqueue_step(d);
+      const int e = use_persist(d) ? enqueue_persistent(d, false, lc) : enqueue_step(d);
       hipError_t ce = hipStreamEndCapture(d->stream, &g);
       if (e) return e;
       TL_TRY(ce);
-      TL_TRY(hipGraphInstantiate(&d->exec_fwd, g, nullptr, nullptr, 0));
+      TL_TRY(hipGraphInstantiate(&d->exec_fwd[lc], g, nullptr, nullptr, 0));
       (void)hipGraphDestroy(g);
     }
-    TL_TRY(hipGraphLaunch(d->exec_fwd, d->stream));
+    TL_TRY(hipGraphLaunch(d->exec_fwd[lc], d->stream));
   } else {
-    r = use_persist(d) ? enqueue_persistent(d, false) : enqueue_step(d);
+    r = use_persist(d) ? enqueue_persistent(d, false, long_ctx(d, pos_h[0])) : enqueue_step(d);
     if (r) return r;
   }
   if (logits_h)
@@ -987,14 +998,14 @@ static int decoder_greedy_once(thallama_decoder* d, const int* token0_h, const i
                                int* tokens_out_h, int sync);
 
 // One greedy step (the step + the argmax that feeds tok/pos) captured as a graph, once.
-static int ensure_greedy_graph(thallama_decoder* d) {
-  if (d->exec) return 0;
+static int ensure_greedy_graph(thallama_decoder* d, int lc) {
+  if (d->exec[lc]) return 0;
   ApiLock lock(api_mu());
   hipGraph_t g = nullptr;
   TL_TRY(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
   int e = 0;
   if (use_persist(d)) {
-    e = enqueue_persistent(d, true);
+    e = enqueue_persistent(d, true, lc);
   } else {
     e = enqueue_step(d);
     if (!e) e = enqueue_argmax(d);
@@ -1002,7 +1013,7 @@ static int ensure_greedy_graph(thallama_decoder* d) {
   hipError_t ce = hipStreamEndCapture(d->stream, &g);
   if (e) return e;
   TL_TRY(ce);
-  TL_TRY(hipGraphInstantiate(&d->exec, g, nullptr, nullptr, 0));
+  TL_TRY(hipGraphInstantiate(&d->exec[lc], g, nullptr, nullptr, 0));
   (void)hipGraphDestroy(g);
   return 0;
 }
@@ -1014,10 +1025,11 @@ static int decoder_step_argmax_once(thallama_decoder* d, const int* token_h, con
   int r = upload_tok_pos(d, token_h, pos_h);
   if (r) return r;
   if (d->use_graph && !d->profile) {
-    if ((r = ensure_greedy_graph(d)) != 0) return r;
-    TL_TRY(hipGraphLaunch(d->exec, d->stream));
+    const int lc = long_ctx(d, pos_h[0]);
+    if ((r = ensure_greedy_graph(d, lc)) != 0) return r;
+    TL_TRY(hipGraphLaunch(d->exec[lc], d->stream));
   } else {
-    r = use_persist(d) ? enqueue_persistent(d, true) : enqueue_step(d);
+    r = use_persist(d) ? enqueue_persistent(d, true, long_ctx(d, pos_h[0])) : enqueue_step(d);
     if (!r && !use_persist(d)) r = enqueue_argmax(d);
     if (r) return r;
   }
@@ -1064,12 +1076,17 @@ static int decoder_greedy_once(thallama_decoder* d, const int* token0_h, const i
   int r = upload_tok_pos(d, token0_h, pos0_h);
   if (r) return r;
   const bool graph = d->use_graph && !d->profile;
-  if (graph && (r = ensure_greedy_graph(d)) != 0) return r;
+  // step i runs at position pos0 + i: captured before the first replay, one graph per instantiation
+  const int lc_first = n_steps > 0 ? long_ctx(d, pos0_h[0]) : 0;
+  const int lc_last = n_steps > 0 ? long_ctx(d, pos0_h[0] + n_steps - 1) : 0;
+  for (int lc = lc_first; graph && lc <= lc_last; ++lc)
+    if ((r = ensure_greedy_graph(d, lc)) != 0) return r;
   for (int i = 0; i < n_steps; ++i) {
+    const int lc = long_ctx(d, pos0_h[0] + i);
     if (graph) {
-      TL_TRY(hipGraphLaunch(d->exec, d->stream));
+      TL_TRY(hipGraphLaunch(d->exec[lc], d->stream));
     } else if (use_persist(d)) {
-      r = enqueue_persistent(d, true);
+      r = enqueue_persistent(d, true, lc);
       if (r) return r;
     } else {
       r = enqueue_step(d);

@@ -65,11 +65,16 @@ constexpr unsigned kSpinLimit = 1u << 18;
 #ifndef PERSIST_ATTN_WIN
 #define PERSIST_ATTN_WIN 1  // fp32: attention units with their keys in LDS windows (attn_unit_win)
 #endif
-// From this many keys on (fp32, batch 1), the attention phase runs twice as many units (key
-// splits) per head: one on each block's control wave and one on streaming wave 1, whose window is
-// the staging strip (free between the QKV and Wo stagings).  One wave keeps at most ~63 KiB of
-// K/V in flight (vmcnt), so at long contexts the phase is latency-bound per unit.
-constexpr int kAttnHelpMinKeys = 512;
+// From kAttnHelpMinKeys keys on (fp32, batch 1; persist.hpp), the attention phase runs twice as
+// many units (key splits) per head: one on each block's control wave and one on streaming wave 1,
+// whose window is the staging strip (free between the QKV and Wo stagings).  One wave keeps at
+// most ~63 KiB of K/V in flight (vmcnt), so at long contexts the phase is latency-bound per unit.
+// The helper lives in its own kernel instantiation (HELP), launched only at such positions: its
+// registers (the streaming wave's slots stay live across the unit) spill 20 B in the shared
+// code, which cost the short-context step 1.2% (profiles/r04/attn_help_ab.txt).
+#ifndef PERSIST_ATTN_HELP
+#define PERSIST_ATTN_HELP 1
+#endif
 #ifndef PERSIST_XCD_SKEW
 #define PERSIST_XCD_SKEW 4
 #endif
@@ -709,7 +714,7 @@ TL_DEVICE void grid_barrier(const PStep& p) {
 
 // The phase sequence as seen by one wave.  ROLE0 = the control wave (epilogues, attention,
 // norm preloads); the other waves stream.  Both execute the same workgroup barriers.
-template <int HS, bool ROLE0, bool Q8>
+template <int HS, bool ROLE0, bool Q8, bool HELP>
 TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xres, float* red,
                       float* rmsw, f4* xs, signed char* xq, float* xsc, float* sqa, float* scr, float* cwb,
                       const uint64_t* etab, unsigned tb, float* awin) {
@@ -750,7 +755,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
             attn_unit_split<HS>(aw, u / p.ang, u % p.ang, p.ang, scr, reinterpret_cast<float*>(xs), p.pad_floats, lane);
         } else {
           // long contexts: twice the splits, the second unit of each block on streaming wave 1
-          const bool help = p.attn_help && p.pos[0] + 1 >= kAttnHelpMinKeys;
+          const bool help = HELP && p.attn_help && p.pos[0] + 1 >= kAttnHelpMinKeys;
           if (help) aw.NS = aw.a.nsplit = 2 * p.NS < kMaxNS ? 2 * p.NS : kMaxNS;
           const int units = p.H * aw.NS;
           for (int u = blockIdx.x; u < units; u += (help ? 2 : 1) * G) {
@@ -796,7 +801,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
       const int kind = ph == nph - 1 ? PK_CLS : ph % 5;
       if (kind == PK_ATTN) {
         if constexpr (!Q8 && PERSIST_ATTN_WIN) {
-          if (p.attn_help && p.pos[0] + 1 >= kAttnHelpMinKeys) {
+          if (HELP && p.attn_help && p.pos[0] + 1 >= kAttnHelpMinKeys) {
             if (sw == 0) {  // the block's second attention unit (control wave: the first)
               AttnWaveParams aw = {};
               aw.a.q = p.xb; aw.a.kc = p.kc; aw.a.vc = p.vc;
@@ -879,7 +884,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
   }
 }
 
-template <int HS, bool Q8>
+template <int HS, bool Q8, bool HELP>
 __global__ void __launch_bounds__(PT) persistent_step_kernel(PStep p) {
   if (p.fault && blockIdx.x == 0) return;  // test hook: a missing block (every wait is bounded)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -904,8 +909,8 @@ __global__ void __launch_bounds__(PT) persistent_step_kernel(PStep p) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const unsigned tb = p.seq[0] << 12;  // tag base of this launch
-  if (wave == 0) phases<HS, true, Q8>(p, wave, lane, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, etab, tb, awin);
-  else phases<HS, false, Q8>(p, wave, lane, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, etab, tb, awin);
+  if (wave == 0) phases<HS, true, Q8, HELP>(p, wave, lane, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, etab, tb, awin);
+  else phases<HS, false, Q8, HELP>(p, wave, lane, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, etab, tb, awin);
 }
 
 constexpr size_t kDynLdsCap = 160 * 1024;  // dynamic LDS per block (gfx950: 160 KiB per CU)
@@ -916,10 +921,11 @@ static size_t lds_bytes(const PStep& p) {
          (p.q8 || !PERSIST_ATTN_WIN ? 0 : (size_t)attn_win_floats(p.hs) * 4);
 }
 
-template <int HS, bool Q8>
-static const void* kfn() { return (const void*)persistent_step_kernel<HS, Q8>; }
+template <int HS, bool Q8, bool HELP = false>
+static const void* kfn() { return (const void*)persistent_step_kernel<HS, Q8, HELP>; }
 static const void* kernel_of(const PStep& p) {
   if (p.q8) return p.hs == 128 ? kfn<128, true>() : kfn<64, true>();
+  if (PERSIST_ATTN_HELP && p.attn_help && p.long_ctx) return p.hs == 128 ? kfn<128, false, true>() : kfn<64, false, true>();
   return p.hs == 128 ? kfn<128, false>() : kfn<64, false>();
 }
 
@@ -994,7 +1000,7 @@ bool persistent_prepare(PStep& p, int ncu, const char** why) {
   }
   if (lds_bytes(p) > kDynLdsCap) return fail("activations do not fit the LDS");
   p.attn_help = 0;
-  if (!p.q8 && PERSIST_ATTN_WIN && p.NS * 2 <= kMaxNS) {  // room for a second attention window in the strip?
+  if (!p.q8 && PERSIST_ATTN_WIN && PERSIST_ATTN_HELP && p.NS * 2 <= kMaxNS) {  // room for a second attention window in the strip?
     const int base = p.pad_floats, need = attn_win_floats(p.hs);
     if (base < need) p.pad_floats = need;
     if (lds_bytes(p) <= kDynLdsCap) p.attn_help = 1;
@@ -1010,7 +1016,8 @@ bool persistent_prepare(PStep& p, int ncu, const char** why) {
     std::lock_guard<std::mutex> lock(mu);
     const unsigned long long bit = dev < 64 ? 1ull << dev : 0ull;
     if (!bit || !(done & bit)) {
-      for (const void* f : {kfn<128, false>(), kfn<64, false>(), kfn<128, true>(), kfn<64, true>()})
+      for (const void* f : {kfn<128, false>(), kfn<64, false>(), kfn<128, true>(), kfn<64, true>(),
+                            kfn<128, false, true>(), kfn<64, false, true>()})
         if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDynLdsCap) != hipSuccess) {
           (void)hipGetLastError();  // (not sticky for the caller's next launch check)
           return fail("cannot raise the dynamic LDS limit");
@@ -1056,14 +1063,9 @@ hipError_t launch_persistent_step(const PStep& p, hipStream_t s, int ncu) {
     void* args[] = {&arg};
     return hipLaunchCooperativeKernel(kernel_of(p), dim3(ncu), dim3(PT), args, (unsigned)lds_bytes(p), s);
   }
-  if (p.q8) {
-    if (p.hs == 128) hipLaunchKernelGGL((persistent_step_kernel<128, true>), dim3(ncu), dim3(PT), lds_bytes(p), s, p);
-    else hipLaunchKernelGGL((persistent_step_kernel<64, true>), dim3(ncu), dim3(PT), lds_bytes(p), s, p);
-  } else {
-    if (p.hs == 128) hipLaunchKernelGGL((persistent_step_kernel<128, false>), dim3(ncu), dim3(PT), lds_bytes(p), s, p);
-    else hipLaunchKernelGGL((persistent_step_kernel<64, false>), dim3(ncu), dim3(PT), lds_bytes(p), s, p);
-  }
-  return hipGetLastError();
+  PStep arg = p;
+  void* args[] = {&arg};
+  return hipLaunchKernel(kernel_of(p), dim3(ncu), dim3(PT), args, lds_bytes(p), s);
 }
 
 }  // namespace tl

@@ -43,6 +43,7 @@ struct PStep {
   int ang;                  // Q8: attention units per head (persistent_prepare)
   int attn_help;            // fp32 batch 1: the staging strip also holds an attention window, so a
                             // streaming wave runs a second attention unit per block at long contexts
+  int long_ctx;             // host: launch the instantiation with that helper (persistent_long_ctx)
   int fault;                // test hook (THALLAMA_OPT_PERSIST_FAULT): block 0 exits at once, as
                             // if the grid were not co-resident; every other wait gives up
   int B;                    // batched step (persist_b.hip): 2..8 sequences; tok / pos / out and every
@@ -61,6 +62,10 @@ bool persistent_prepare(PStep& p, int ncu, const char** why);
 hipError_t launch_persistent_step(const PStep& p, hipStream_t s, int ncu);
 // True if launch_persistent_step uses a cooperative launch (co-residency guaranteed).
 bool persistent_cooperative();
+// fp32 batch 1: from this many keys on the step runs the attention helper (persist.hip), so the
+// caller sets PStep::long_ctx and keeps one captured graph per setting
+constexpr int kAttnHelpMinKeys = 512;
+inline bool persistent_long_ctx(int pos) { return pos + 1 >= kAttnHelpMinKeys; }
 // The same for 2..8 sequences with fp32 weights (persist_b.hip; p.B set).
 bool persistent_prepare_b(PStep& p, int ncu, const char** why);
 hipError_t launch_persistent_step_b(const PStep& p, hipStream_t s, int ncu);
