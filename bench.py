@@ -434,7 +434,8 @@ def main(argv=None):
         # HBM traffic of the same kernel from the committed rocprofv3 PMC passes (FETCH_SIZE and
         # WRITE_SIZE in separate runs, gfx950 FETCH_SIZE x2 correction): profiles/*pmc_traffic*.json
         pmc = {}
-        for fn in (f"r03_pmc_traffic_{args.dtype}_b{B}.json", "r02_pmc_traffic_int8.json" if q8 else
+        for fn in (f"r04_pmc_traffic_{args.dtype}_b{B}.json", f"r03_pmc_traffic_{args.dtype}_b{B}.json",
+                   "r02_pmc_traffic_int8.json" if q8 else
                    "r02_pmc_traffic.json"):
             try:
                 with open(os.path.join(REPO, "profiles", fn)) as f:
