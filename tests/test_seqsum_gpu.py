@@ -53,7 +53,7 @@ def test_wave_seqsum_bitexact(gpu, kind, n):
 
 
 @pytest.mark.parametrize("kind", ["gauss_sq", "ints_sq", "softmax"])
-@pytest.mark.parametrize("n", [4096, 768, 200])
+@pytest.mark.parametrize("n", [4096, 4095, 3000, 2304, 2049, 768, 200])
 def test_wave_seqsum_reg_bitexact(gpu, kind, n):
     """The register form (n <= 4096; the norm and softmax sums of the int8 step) is the chain too;
     it also reports clock cycles per call (printed)."""
