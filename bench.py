@@ -13,10 +13,14 @@ Workloads (one "step" = one pass of the hot path over one batch of synthetic inp
 * ``cli`` (default at N > 1; BASELINE.json configs[4]): the drop-in's own multi-GPU path — the
   CLI build/apps/llama in test mode (src/llama.cpp:891-1083: one host thread per GPU, weights
   uploaded once and RCCL-broadcast over xGMI) over the reference's assets/in/gen_in_64.txt
-  prompts: 8 per GPU (--prompts-per-gpu; all 64 at N = 8), 8 slots per GPU, greedy (-g 1),
-  prompts prefilled, each request to position 255 or EOS/BOS.  A step is one pass over the job;
-  value = the reference's token count (sum of pos - 1 over requests, src/llama.cpp:1062) / the
-  CLI's serve time.  The output file is compared with a committed one-process fixture.
+  prompts: 8 per GPU (--prompts-per-gpu; all 64 at N = 8), greedy (-g 1), prompts prefilled,
+  each request to position 255 or EOS/BOS.  A step is one pass over the job; value = the
+  reference's token count (sum of pos - 1 over requests, src/llama.cpp:1062) / the CLI's serve
+  time.  value runs ONE slot per GPU (-b 1), the per-GPU work of the N = 1 line, so the driver's
+  per-N values form a weak-scaling curve; the same job at 8 slots per GPU (-b 8, the batched
+  form) rides along as "batched".  Each output file is compared with a committed one-process
+  fixture of its slot count.  At N = 1 the decode line carries both CLI runs on the one GPU
+  ("cli_1gpu"), the per-GPU base of the N > 1 numbers.
 * ``requests``: the same job through a torch.distributed process-per-GPU harness
   (hip_llama_cpp_amd/dist.py over the HIP decoder's native callbacks) — a cross-check of the CLI.
 
@@ -54,6 +58,12 @@ PROMPTS = os.path.join(GOLDEN, "gen_in_64.txt")  # the reference's assets/in/gen
 TOKENIZER = os.path.join(GOLDEN, "tokenizer.bin")  # the reference's assets/tokenizer.bin
 
 
+def fixture_path(mname, dtype, B):
+    """The committed output file of the request job at B slots per GPU (one process, one GPU,
+    all 64 prompts; bench.py --workload requests --batch B --write-fixture)."""
+    return os.path.join(GOLDEN, f"bench_requests_{mname}_{dtype}_greedy{'' if B == 8 else f'_b{B}'}.json")
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -80,6 +90,7 @@ def parse_args(argv):
                     help="multi-launch step instead of the one-launch persistent step")
     ap.add_argument("--no-long", action="store_true", help="skip the positions 1792..2047 line")
     ap.add_argument("--no-requests-point", action="store_true", help="skip the 1-GPU request-workload point")
+    ap.add_argument("--no-cli-point", action="store_true", help="skip the 1-GPU CLI runs (-b 1 and -b 8)")
     ap.add_argument("--host-argmax", action="store_true",
                     help="requests: greedy sampling on the host from copied logits (the reference's way)")
     ap.add_argument("--write-fixture", action="store_true",
@@ -184,103 +195,114 @@ def plumbing(args, world, rank):
 
 
 # ---------------------------------------------------------------- --workload cli (configs[4])
+def cli_serve(args, world, B, passes, warmup):
+    """One run of the drop-in CLI (build/apps/llama, app/run.cpp — the reference's
+    test_data_parallelism, src/llama.cpp:891-1083: one host thread per GPU, B slots per thread, one
+    weight image made on GPU 0 and RCCL-broadcast over xGMI) serving the first prompts_per_gpu x N
+    prompts of gen_in_64.txt greedily (-g 1), each request to position decode_len - 1 or EOS/BOS.
+    The weights are the synthetic model made on GPU 0 ("synth:" spec, no 27 GB file).  Started as
+    a child process over GPUs 0..N-1; it serves the file warmup + passes times on the same
+    resident weights (THALLAMA_PASSES).  Returns tokens / serve time of the timed passes (the CLI's
+    own clock, weights already in HBM) and whether the output file equals the committed
+    one-process fixture of B slots, byte for byte."""
+    cfg_t, shared, mname = MODELS[args.model]
+    q8 = args.dtype == "int8"
+    T = args.decode_len
+    n = args.prompts_per_gpu * world
+    if n > 64:
+        raise SystemExit(f"{n} prompts > the 64 of gen_in_64.txt")
+    exe = os.path.join(REPO, "build", "apps", "llama")
+    if not os.path.exists(exe):
+        raise SystemExit(f"bench.py: {exe} not built (make -C hip_llama.cpp_amd)")
+    dims = list(cfg_t)
+    dims[5] = dims[5] if shared else -dims[5]
+    spec = "synth:" + ",".join(str(v) for v in dims) + f":{SEED}" + (f":q8:{args.group_size}" if q8 else "")
+    wd = tempfile.mkdtemp(prefix=".bench_cli_", dir=REPO)
+    req = write_requests(read_prompts(PROMPTS, n), wd)
+    out = os.path.join(wd, "out.txt")
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if "HIP_VISIBLE_DEVICES" not in env and "ROCR_VISIBLE_DEVICES" not in env:
+        env["HIP_VISIBLE_DEVICES"] = ",".join(str(i) for i in range(world))
+    if args.cli_replicas:
+        env["THALLAMA_REPLICAS"] = str(args.cli_replicas)
+    env["THALLAMA_PASSES"] = str(warmup + passes)
+    env["THALLAMA_TEST_STEPS"] = str(T)
+    cmd = [exe, spec, "-m", "test", "-f", req, "-o", out, "-b", str(B), "-g", "1", "-z", TOKENIZER]
+    log("bench.py: " + " ".join(cmd))
+    t0 = time.perf_counter()
+    p = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True)
+    wall = time.perf_counter() - t0
+    if p.returncode != 0:
+        log(p.stdout[-4000:], p.stderr[-4000:])
+        raise SystemExit(f"bench.py: the CLI failed ({p.returncode})")
+    runs = [(int(ln.split()[3]), float(ln.split()[5])) for ln in p.stdout.splitlines() if ln.startswith("pass ")]
+    if not runs:  # one pass: the reference's own summary lines
+        tot = [ln for ln in p.stdout.splitlines() if ln.startswith("Total achieved token:")]
+        el = [ln for ln in p.stdout.splitlines() if ln.startswith("elapsed time(s):")]
+        runs = [(int(tot[-1].split()[-1]), float(el[-1].split()[2].rstrip(",")))]
+    timed_p = runs[warmup:] or runs
+    tokens = sum(t for t, _ in timed_p)
+    secs = sum(x for _, x in timed_p)
+    load = next((float(ln.split()[-1]) for ln in p.stdout.splitlines() if ln.startswith("Load model time")), None)
+    with open(out, "rb") as f:
+        got = f.read()
+    fx_path = fixture_path(mname, args.dtype, B)
+    match = None
+    if os.path.exists(fx_path):
+        with open(fx_path) as f:
+            fx = json.load(f)
+        if fx.get("decode_len") == T and fx.get("seed") == SEED and len(fx["outputs"]) >= n:
+            want = f"{n}\n".encode() + b"".join(o.encode("utf-8", "surrogateescape") + b"\n" for o in fx["outputs"][:n])
+            match = got == want
+    for f_ in (req, out):
+        os.remove(f_)
+    os.rmdir(wd)
+    return {"value": round(tokens / secs, 3), "unit": "tok/s", "slots_per_gpu": B, "prompts": n,
+            "seconds_per_pass": round(secs / len(timed_p), 4), "tokens_per_pass": timed_p[0][0],
+            "cmd": " ".join(os.path.relpath(c, REPO) if c.startswith(REPO) else c for c in cmd),
+            "passes": [{"tokens": t, "seconds": x} for t, x in runs], "warmup_passes": warmup,
+            "load_s": load, "wall_s": round(wall, 2), "replicas": args.cli_replicas or world,
+            "output_matches_fixture": match,
+            "fixture": os.path.relpath(fx_path, REPO) if os.path.exists(fx_path) else None,
+            "output_sha": hashlib.sha256(got).hexdigest()[:16]}
+
+
 def cli_run(args, world, rank):
-    """BASELINE.json configs[4] through the drop-in's OWN multi-GPU path: the CLI
-    (build/apps/llama, app/run.cpp — the reference's test_data_parallelism, src/llama.cpp:891-1083:
-    one host thread per GPU, one slot batch per thread, one weight upload then an RCCL broadcast
-    over xGMI) serving the first prompts_per_gpu x N prompts of gen_in_64.txt greedily (-g 1) with
-    B slots per GPU, each request to position decode_len - 1 or EOS/BOS.  The weights are the
-    synthetic model made on GPU 0 ("synth:" spec, no 27 GB file).  Rank 0 starts the CLI as a child
-    process over GPUs 0..N-1 before anything here touches a GPU; other ranks only wait (gloo).
-    The CLI serves the file warmup + steps times on the same resident weights (THALLAMA_PASSES);
-    value = tokens of the timed passes / their serve time (the CLI's own clock, weights already
-    in HBM); the output file is compared byte for byte with the committed one-process fixture."""
+    """BASELINE.json configs[4] through the drop-in's OWN multi-GPU path (cli_serve): rank 0 starts
+    the CLI over GPUs 0..N-1 before anything here touches a GPU; other ranks only wait (gloo).
+    value: one slot per GPU (-b 1, the per-GPU work of the N = 1 decode line, so the per-N values
+    are a weak-scaling curve); "batched": the same job at 8 slots per GPU (-b 8), unless --batch
+    picks the slot count of value."""
     import torch.distributed as dist
     if world > 1:
         dist.init_process_group(backend="gloo")
     res = None
     if rank == 0:
         cfg_t, shared, mname = MODELS[args.model]
-        q8 = args.dtype == "int8"
-        T, B = args.decode_len, args.batch or 8
-        n = args.prompts_per_gpu * world
-        if n > 64:
-            raise SystemExit(f"{n} prompts > the 64 of gen_in_64.txt")
-        exe = os.path.join(REPO, "build", "apps", "llama")
-        if not os.path.exists(exe):
-            raise SystemExit(f"bench.py: {exe} not built (make -C hip_llama.cpp_amd)")
-        dims = list(cfg_t)
-        dims[5] = dims[5] if shared else -dims[5]
-        spec = "synth:" + ",".join(str(v) for v in dims) + f":{SEED}" + (f":q8:{args.group_size}" if q8 else "")
-        wd = tempfile.mkdtemp(prefix=".bench_cli_", dir=REPO)
-        req = write_requests(read_prompts(PROMPTS, n), wd)
-        out = os.path.join(wd, "out.txt")
-        env = dict(os.environ)
-        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        if "HIP_VISIBLE_DEVICES" not in env and "ROCR_VISIBLE_DEVICES" not in env:
-            env["HIP_VISIBLE_DEVICES"] = ",".join(str(i) for i in range(world))
-        if args.cli_replicas:
-            env["THALLAMA_REPLICAS"] = str(args.cli_replicas)
-        env["THALLAMA_PASSES"] = str(args.warmup + args.steps)
-        env["THALLAMA_TEST_STEPS"] = str(T)
-        cmd = [exe, spec, "-m", "test", "-f", req, "-o", out, "-b", str(B), "-g", "1", "-z", TOKENIZER]
-        log("bench.py: " + " ".join(cmd))
-        t0 = time.perf_counter()
-        p = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True)
-        wall = time.perf_counter() - t0
-        if p.returncode != 0:
-            log(p.stdout[-4000:], p.stderr[-4000:])
-            raise SystemExit(f"bench.py: the CLI failed ({p.returncode})")
-        passes = [(int(ln.split()[3]), float(ln.split()[5])) for ln in p.stdout.splitlines()
-                  if ln.startswith("pass ")]
-        if not passes:  # one pass: the reference's own summary lines
-            tot = [ln for ln in p.stdout.splitlines() if ln.startswith("Total achieved token:")]
-            el = [ln for ln in p.stdout.splitlines() if ln.startswith("elapsed time(s):")]
-            passes = [(int(tot[-1].split()[-1]), float(el[-1].split()[2].rstrip(",")))]
-        timed_p = passes[args.warmup:] or passes
-        tokens = sum(t for t, _ in timed_p)
-        secs = sum(x for _, x in timed_p)
-        load = next((float(ln.split()[-1]) for ln in p.stdout.splitlines() if ln.startswith("Load model time")), None)
-        with open(out, "rb") as f:
-            got = f.read()
-        fx_path = os.path.join(GOLDEN, f"bench_requests_{mname}_{args.dtype}_greedy.json")
-        match = None
-        if os.path.exists(fx_path):
-            with open(fx_path) as f:
-                fx = json.load(f)
-            if fx.get("decode_len") == T and fx.get("seed") == SEED and len(fx["outputs"]) >= n:
-                want = f"{n}\n".encode() + b"".join(o.encode("utf-8", "surrogateescape") + b"\n"
-                                                      for o in fx["outputs"][:n])
-                match = got == want
-        # algorithmic bytes: every decode step of a GPU reads the weights once for its B slots plus
-        # each slot's K/V rows; requests here run from their prompt to T - 1
+        T = args.decode_len
+        B = args.batch or 1
+        r = cli_serve(args, world, B, args.steps, args.warmup)
+        batched = None if args.batch else cli_serve(args, world, 8, args.steps, args.warmup)
         wbytes = 4.0 * (cfg_t[2] * (2 * cfg_t[0] ** 2 + 2 * cfg_t[0] * cfg_t[0] * cfg_t[4] // cfg_t[3]
                                     + 3 * cfg_t[0] * cfg_t[1]) + cfg_t[5] * cfg_t[0])
         res = {"metric": "decode tokens/sec (greedy, whole model) + achieved HBM GB/s fraction",
-               "value": round(tokens / secs, 3), "unit": "tok/s", "n_gpus": world, "steps": len(timed_p),
-               "warmup": args.warmup, "ms_per_step": round(1e3 * secs / len(timed_p), 3),
+               "value": r["value"], "unit": "tok/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(1e3 * r["seconds_per_pass"], 3),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
                "data": "synthetic weights (random init, seed 20240224, made on GPU 0); prompts: the reference's "
                        "gen_in_64.txt",
                "config": {"workload": f"{mname} {args.dtype} drop-in CLI test mode (build/apps/llama -m test -g 1 "
-                                      f"-b {B}; src/llama.cpp:891-1083), {n} prompts of gen_in_64.txt "
+                                      f"-b {B}; src/llama.cpp:891-1083), {r['prompts']} prompts of gen_in_64.txt "
                                       f"({args.prompts_per_gpu} per GPU, one host thread + RCCL-broadcast replica per "
                                       f"GPU), each request to position {T - 1} or EOS/BOS",
-                          "model": mname, "global_batch": n, "slots_per_gpu": B, "seq_len": cfg_t[6], "decode_len": T,
-                          "parallelism": f"prompt-dp{world} (threads + RCCL broadcast)"},
-               "cli": {"cmd": " ".join(os.path.relpath(c, REPO) if c.startswith(REPO) else c for c in cmd),
-                       "passes": [{"tokens": t, "seconds": x} for t, x in passes],
-                       "load_s": load, "wall_s": round(wall, 2), "replicas": args.cli_replicas or world,
-                       "output_matches_fixture": match,
-                       "fixture": os.path.relpath(fx_path, REPO) if os.path.exists(fx_path) else None,
-                       "output_sha": hashlib.sha256(got).hexdigest()[:16]},
+                          "model": mname, "global_batch": r["prompts"], "slots_per_gpu": B, "seq_len": cfg_t[6],
+                          "decode_len": T, "parallelism": f"prompt-dp{world} (threads + RCCL broadcast)"},
+               "cli": r, "batched": batched,
                "roofline": None,
                "roofline_note": "the CLI runs in a child process: per-kernel HIP events are in the N = 1 decode line; "
-                                f"weights {wbytes / 1e9:.2f} GB read once per step for {B} slots",
+                                f"weights {wbytes / 1e9:.2f} GB read once per step for the slots of a GPU",
                "cpu_baseline": None}
-        for f_ in (req, out):
-            os.remove(f_)
-        os.rmdir(wd)
     if world > 1:
         dist.barrier()
     if rank == 0:
@@ -310,6 +332,12 @@ def main(argv=None):
     workload = args.workload or ("decode" if world == 1 else "cli")
     if workload == "cli":
         return cli_run(args, world, rank)
+    # the 1-GPU base of the N > 1 CLI numbers, before this process touches the GPU (7B fp32, the
+    # job whose fixtures are committed)
+    cli_point = None
+    if (workload == "decode" and world == 1 and not args.no_cli_point and args.model == "7b" and
+            args.dtype == "f32" and args.decode_len == 256 and not args.batch):
+        cli_point = {"b1": cli_serve(args, 1, 1, 2, 1), "b8": cli_serve(args, 1, 8, 2, 1)}
 
     import torch
     import torch.distributed as dist
@@ -511,7 +539,7 @@ def main(argv=None):
         res = None
         if rank == 0:
             outs = [o.decode("utf-8", "replace") for o in outs]
-            fx_path = os.path.join(GOLDEN, f"bench_requests_{mname}_{args.dtype}_greedy.json")
+            fx_path = fixture_path(mname, args.dtype, B)
             match, fx_n = None, 0
             if fixture_write:
                 with open(fx_path, "w") as f:
@@ -731,6 +759,7 @@ def main(argv=None):
                 "reference_tokens": golden,
                 "long_context": long_ctx,
                 "requests_1gpu": req_point,
+                "cli_1gpu": cli_point,
                 "kernels": prof, "kernels_multilaunch": prof_ml,
                 "cpu_baseline": cpu,
                 "init_s": round(t_init, 2), "broadcast_s": round(t_bcast, 2),
