@@ -648,20 +648,56 @@ TL_DEVICE void attn_unit_split(const AttnWaveParams& w, int h, int c, int NG, fl
 // attn_unit (same records and tickets).  win: attn_win_floats(HS) floats of LDS.
 __host__ __device__ constexpr int attn_win_floats(int hs) { return 2 * 64 * hs + 2 * hs; }
 
+// The key range of attn_unit_win's unit (b, h, split s): [k0, k1) of T keys, the cached ones
+// [k0, ke); live = the unit has keys.
+struct WinUnit {
+  int b, h, s, T, nact, k0, k1, ke;
+  bool live;
+};
+TL_DEVICE WinUnit win_unit(const AttnWaveParams& w, int unit) {
+  const AttnParams& p = w.a;
+  const int BH = w.B * p.n_heads;
+  WinUnit u;
+  u.s = unit / BH;
+  const int bh = unit % BH;
+  u.b = bh / p.n_heads;
+  u.h = bh % p.n_heads;
+  u.T = p.pos[u.b] + 1;
+  u.nact = min(w.NS, (u.T + 15) / 16);  // live units for this (b, h): >= 16 keys each
+  u.live = u.s < u.nact;
+  u.k0 = (int)((long long)u.T * u.s / u.nact);
+  u.k1 = (int)((long long)u.T * (u.s + 1) / u.nact);
+  u.ke = min(u.k1, u.T - 1);  // row T-1 comes from the granules
+  return u;
+}
+
+// The DMAs of one round of attn_unit_win: n K rows (or, with v, V rows) from t0 into the window.
+// Units of more than one 64-key round issue exactly PC + 64 / RPI (= 2 PC) wave-instructions per
+// round whatever n (lanes past n re-read row t0 into slots nothing reads), so the unit's waits can
+// count them; a single-round unit issues only its n rows.
+template <int HS>
+TL_DEVICE void win_issue(const float* base, int kv_dim, int t0, int n, bool multi, float* dst, int lane) {
+  constexpr int PC = HS / 4;     // 16-B pieces per row
+  constexpr int RPI = 256 / HS;  // rows per 1-KiB DMA instruction
+  const int kq = lane / PC, pc = lane % PC;
+  const int ni = multi ? 64 / RPI : (n + RPI - 1) / RPI;
+#pragma unroll 4
+  for (int j = 0; j < ni; ++j) {
+    const int kl = j * RPI + kq;  // this lane's row in the round
+    if (multi || kl < n) dma16(base + (long long)(t0 + (kl < n ? kl : 0)) * kv_dim + 4 * pc, dst + j * 256);
+  }
+}
+
 template <int HS>
 TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int lane) {
   constexpr int VPL = HS / 64;
   constexpr int PC = HS / 4;     // 16-B pieces per row
   constexpr int RPI = 256 / HS;  // V rows per 1-KiB DMA instruction
   const AttnParams& p = w.a;
-  const int BH = w.B * p.n_heads;
-  const int s = unit / BH, bh = unit % BH;
-  const int b = bh / p.n_heads, h = bh % p.n_heads;
-  const int T = p.pos[b] + 1;
-  const int nact = min(w.NS, (T + 15) / 16);  // live units for this (b, h): >= 16 keys each
-  if (s >= nact) return;
-  const int k0 = (int)((long long)T * s / nact), k1 = (int)((long long)T * (s + 1) / nact);
-  const int tc = T - 1;  // cached rows [0, T-1); row T-1 from the granules
+  const WinUnit u = win_unit(w, unit);
+  if (!u.live) return;
+  const int s = u.s, b = u.b, h = u.h, T = u.T, nact = u.nact, k0 = u.k0, k1 = u.k1, ke = u.ke;
+  const int bh = b * p.n_heads + h;
   const int kvh = h / p.kv_mul;
   const float* kbase = p.kc + (long long)b * p.kv_b_stride + p.kv_l_off + (long long)kvh * HS;
   const float* vbase = p.vc + (long long)b * p.kv_b_stride + p.kv_l_off + (long long)kvh * HS;
@@ -669,7 +705,6 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
   float* vw = kw + 64 * HS;     // [64][HS]
   float* qs = vw + 64 * HS;     // q [HS]
   float* kn = qs + HS;          // k row T-1 [HS]
-  const int ke = min(k1, tc);   // cached keys of this unit: [k0, ke)
   // Units of more than one 64-key round (long contexts) issue a round's K and V rows as exactly
   // PC + 64 / RPI (= 2 PC) wave-instructions whatever its key count n (lanes past n re-read row
   // t0 into slots nothing reads), so the waits below can count them: the next round's K rows land
@@ -680,23 +715,8 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
   // ab.json); the lane-per-key dot below walks its row from piece `lane` on, so the 16 lanes of a
   // read hit 16 different bank groups
   const bool multi = ke - k0 > 64;
-  auto issue_k = [&](int t0, int n) {
-    const int kq = lane / PC, pc = lane % PC;
-    const int ni = multi ? 64 / RPI : (n + RPI - 1) / RPI;
-#pragma unroll 4
-    for (int j = 0; j < ni; ++j) {
-      const int kl = j * RPI + kq;  // this lane's key in the round
-      if (multi || kl < n) dma16(kbase + (long long)(t0 + (kl < n ? kl : 0)) * p.kv_dim + 4 * pc, kw + j * 256);
-    }
-  };
-  auto issue_v = [&](int t0, int n) {
-    const int ni = multi ? 64 / RPI : (n + RPI - 1) / RPI;
-#pragma unroll 4
-    for (int j = 0; j < ni; ++j) {
-      const int r = j * RPI + lane / PC;
-      if (multi || r < n) dma16(vbase + (long long)(t0 + (r < n ? r : 0)) * p.kv_dim + (lane % PC) * 4, vw + j * 256);
-    }
-  };
+  auto issue_k = [&](int t0, int n) { win_issue<HS>(kbase, p.kv_dim, t0, n, multi, kw, lane); };
+  auto issue_v = [&](int t0, int n) { win_issue<HS>(vbase, p.kv_dim, t0, n, multi, vw, lane); };
   static_assert(64 / RPI == PC, "K and V rounds are the same instruction count");
   auto wait_all_but_round_half = [] {  // every DMA but the last PC instructions landed
     if constexpr (PC == 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
@@ -736,6 +756,7 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
     }
   }
   wave_lds_fence();
+  if (w.ts && lane == 0) w.ts[0] = __builtin_amdgcn_s_memrealtime();  // (diagnostics: q / k / v granules in)
   const float rs = sqrtf((float)HS);
   const f4* q4 = reinterpret_cast<const f4*>(qs);
   float m = -3.402823466e+38f, l = 0.f;
@@ -792,6 +813,7 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
     wave_lds_fence();  // the V window's reads are done
     if (more) issue_v(t0 + 64, min(64, ke - t0 - 64));
   }
+  if (w.ts && lane == 0) w.ts[1] = __builtin_amdgcn_s_memrealtime();  // (diagnostics: cached keys folded)
   if (last) {  // key T-1: every lane computes its score (one key), lane 0's counts
     const float sc = dot(kn, 1);
     // fold one key whose V row is vn (in registers): the same arithmetic inline
@@ -805,10 +827,12 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
     m = mn;
   }
   wave_lds_fence();  // the window is rewritten by the block's next unit
+  if (w.ts && lane == 0) w.ts[3] = __builtin_amdgcn_s_memrealtime();  // (diagnostics: unit computed)
   if (nact == 1) {
 #pragma unroll
     for (int c = 0; c < VPL; ++c) o[c] = __fdiv_rn(o[c], l);
     publish_head<HS>(w, b, h, o, lane);
+    if (w.ts && lane == 0) w.ts[2] = __builtin_amdgcn_s_memrealtime();  // (diagnostics: head published)
     return;
   }
   // publish this unit's partial (write-through), drain, take a ticket; the last unit combines
@@ -850,6 +874,7 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
 #pragma unroll
   for (int c = 0; c < VPL; ++c) acc[c] = __fdiv_rn(acc[c], L);
   publish_head<HS>(w, b, h, acc, lane);
+  if (w.ts && lane == 0) w.ts[2] = __builtin_amdgcn_s_memrealtime();  // (diagnostics: head combined, published)
   if (lane == 0) __hip_atomic_store(w.cnt + bh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 

@@ -616,7 +616,9 @@ TL_DEVICE float2 rope_cs(const PStep& p, int row) {
 // (a table read at the epilogue put one L2 round trip on every layer's critical path).
 // xres: this block's slice of the residual stream x (rows i0.. of the dim-row phases, the
 // same slice for Wo and W2), kept in LDS so the residual add never re-reads x.
-TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const float* res, float* xres, int lane,
+// int8: the body with the phase kind read at run time (the per-kind instantiations below cost the
+// int8 step 0.6-0.8%: profiles/r04/epilogue_kind_ab.txt).
+TL_DEVICE void epilogue_rt(const PDesc& d, const PGeo& g, const PStep& p, const float* res, float* xres, int lane,
                         int l, float2 cs0, const float* pbuf, const uint64_t* etab) {
   unsigned long long best = 0;
   for (int it = lane; it < g.ni; it += 64) {
@@ -676,6 +678,86 @@ TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const flo
   }
 }
 
+// fp32: one instantiation per phase kind (KIND): the body with the kind read at run time was
+// ~200 scalar-heavy instructions (branches, spilled SGPRs) before the first row value, on every
+// hand-off's critical path (epilogues 2.9 / 1.4 / 1.4 / 1.3 -> 2.1 / 0.4 / 0.7 / 0.6 us for QKV /
+// Wo / W1-W3 / W2; 7B +1.0-1.4%, 110M +1.9%, profiles/r04/epilogue_kind_ab.txt).
+template <int KIND>
+TL_DEVICE void epilogue_k(const PDesc& d, const PGeo& g, const PStep& p, const float* res, float* xres, int lane,
+                          int l, float2 cs0, const uint64_t* etab) {
+  constexpr int kind = KIND, rpi = KIND == PK_QKV || KIND == PK_UP ? 2 : 1;
+  unsigned long long best = 0;
+  for (int it = lane; it < g.ni; it += 64) {
+    float v[2] = {0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < rpi; ++r) {
+      float s;
+      {
+        const float* rr = res + (it * rpi + r) * g.nch;
+        s = rr[0];
+        for (int c = 1; c < g.nch; ++c) s = __fadd_rn(s, rr[c]);
+      }
+      v[r] = s;
+    }
+    if (p.trace && it == 0)  // (diagnostics: the first item's row values are computed)
+      p.trace[((long long)blockIdx.x * (5 * p.L + 1) + (kind == PK_CLS ? 5 * p.L : 5 * l + kind)) * kTraceSlots + 12] =
+          __builtin_amdgcn_s_memrealtime();
+    const int item = g.i0 + it;
+    if (kind == PK_CLS) {
+      p.logits[item] = v[0];  // read by the host after the launch only
+      const unsigned long long k = argmax_pack(v[0], item);
+      best = k > best ? k : best;
+    } else if (kind == PK_WO || kind == PK_DOWN) {
+      xres[it] = __fadd_rn(xres[it], v[0]);  // residual (src/seq.cpp:139-141, 163-166)
+      st8_sc1(d.gout + item, gran(d.tag_out, xres[it]));
+      if (kind == PK_DOWN && l == p.L - 1) p.x[item] = xres[it];  // final residual stream (state)
+    } else if (kind == PK_UP) {
+      st8_sc1(d.gout + item, gran(d.tag_out, silu_mul_tab(v[0], v[1], etab)));
+    } else {  // PK_QKV: RoPE (src/seq.cpp:86-101), q / k_new / v_new granules, KV-cache row
+      const int row = 2 * item;
+      const int pb = p.pos[0];
+      float a0 = v[0], a1 = v[1];
+      if (row < p.dim + p.kvd) {
+        const float2 cs = it == lane ? cs0 : rope_cs(p, row);
+        const float r0 = __fsub_rn(__fmul_rn(a0, cs.x), __fmul_rn(a1, cs.y));
+        const float r1 = __fadd_rn(__fmul_rn(a0, cs.y), __fmul_rn(a1, cs.x));
+        a0 = r0; a1 = r1;
+      }
+      st_gran2(rsrc_of(d.gout), (unsigned)row * 8u, d.tag_out, a0, a1);
+      if (row >= p.dim) {  // the cache row for later steps (this launch reads the granules)
+        int rk = row - p.dim;
+        float* base = p.kc;
+        if (rk >= p.kvd) { rk -= p.kvd; base = p.vc; }
+        *reinterpret_cast<float2*>(base + ((long long)l * p.S + pb) * p.kvd + rk) = make_float2(a0, a1);
+      }
+    }
+  }
+  if (kind == PK_CLS) {
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long other = __shfl_xor(best, o, 64);
+      best = other > best ? other : best;
+    }
+    if (lane == 0) st8_sc1(p.bmax + blockIdx.x, best);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drained before the final arrival
+  }
+}
+
+template <bool Q8>
+TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const float* res, float* xres, int lane,
+                        int l, float2 cs0, const float* pbuf, const uint64_t* etab) {
+  if constexpr (Q8) {
+    epilogue_rt(d, g, p, res, xres, lane, l, cs0, pbuf, etab);
+    return;
+  }
+  switch (d.kind) {
+    case PK_QKV: epilogue_k<PK_QKV>(d, g, p, res, xres, lane, l, cs0, etab); break;
+    case PK_WO: epilogue_k<PK_WO>(d, g, p, res, xres, lane, l, cs0, etab); break;
+    case PK_UP: epilogue_k<PK_UP>(d, g, p, res, xres, lane, l, cs0, etab); break;
+    case PK_DOWN: epilogue_k<PK_DOWN>(d, g, p, res, xres, lane, l, cs0, etab); break;
+    default: epilogue_k<PK_CLS>(d, g, p, res, xres, lane, l, cs0, etab); break;
+  }
+}
+
 // Sharded-counter grid barrier (the final one only).  Callers have drained every storing
 // wave.  One lane per block adds to its shard; lanes 0..7 of wave 0 poll the eight shards.
 TL_DEVICE void grid_barrier(const PStep& p) {
@@ -729,23 +811,30 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
     preload_rms(p.L > 0 ? p.rms_att : p.rms_final, p.dim, rmsw, lane);
     if (lane == 0) *ctr = 0u;
     __syncthreads();  // first norm weights preloaded
+    // the attention units of layer l (fp32 at long contexts: twice the key splits, the helper)
+    const bool help = !Q8 && HELP && p.attn_help && p.pos[0] + 1 >= kAttnHelpMinKeys;
+    auto attn_params = [&](int l) {
+      AttnWaveParams aw = {};
+      aw.a.q = p.xb; aw.a.kc = p.kc; aw.a.vc = p.vc;  // (q comes from the granules)
+      aw.a.kv_b_stride = (long long)p.L * p.S * p.kvd;
+      aw.a.kv_l_off = (long long)l * p.S * p.kvd;
+      aw.a.pos = p.pos; aw.a.out = p.xb; aw.a.part = p.part;
+      aw.a.dim = p.dim; aw.a.kv_dim = p.kvd; aw.a.head_size = HS; aw.a.n_heads = p.H;
+      aw.a.kv_mul = p.kv_mul; aw.a.seq_len = p.S; aw.a.nsplit = p.NS; aw.a.min_chunk = 16;
+      aw.cnt = p.tickets + (long long)l * p.H; aw.B = 1; aw.NS = p.NS;
+      if (help) aw.NS = aw.a.nsplit = 2 * p.NS < kMaxNS ? 2 * p.NS : kMaxNS;
+      aw.gqkv = p.gqkv; aw.gout = p.gxb;
+      aw.gsc = p.gsc; aw.etab = etab;
+      aw.tag_in = tb + 5u * l + 1; aw.tag_out = tb + 5u * l + 2; aw.err = p.err;
+      return aw;
+    };
     for (int ph = 0; ph < nph; ++ph) {
       const int l = ph / 5;
       const int kind = ph == nph - 1 ? PK_CLS : ph % 5;
       TRACE(0);
       if (kind == PK_ATTN) {
         // one wave per (head, key-split) unit: unit u on block u % G
-        AttnWaveParams aw = {};
-        aw.a.q = p.xb; aw.a.kc = p.kc; aw.a.vc = p.vc;  // (q comes from the granules)
-        aw.a.kv_b_stride = (long long)p.L * p.S * p.kvd;
-        aw.a.kv_l_off = (long long)l * p.S * p.kvd;
-        aw.a.pos = p.pos; aw.a.out = p.xb; aw.a.part = p.part;
-        aw.a.dim = p.dim; aw.a.kv_dim = p.kvd; aw.a.head_size = HS; aw.a.n_heads = p.H;
-        aw.a.kv_mul = p.kv_mul; aw.a.seq_len = p.S; aw.a.nsplit = p.NS; aw.a.min_chunk = 16;
-        aw.cnt = p.tickets + (long long)l * p.H; aw.B = 1; aw.NS = p.NS;
-        aw.gqkv = p.gqkv; aw.gout = p.gxb;
-        aw.gsc = p.gsc; aw.etab = etab;
-        aw.tag_in = tb + 5u * l + 1; aw.tag_out = tb + 5u * l + 2; aw.err = p.err;
+        AttnWaveParams aw = attn_params(l);
         aw.ts = p.trace ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots + 8 : nullptr;
         if constexpr (Q8) {
           // int8: runq's attention bit for bit, each head split over p.ang units (attention.hpp
@@ -755,8 +844,6 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
             attn_unit_split<HS>(aw, u / p.ang, u % p.ang, p.ang, scr, reinterpret_cast<float*>(xs), p.pad_floats, lane);
         } else {
           // long contexts: twice the splits, the second unit of each block on streaming wave 1
-          const bool help = HELP && p.attn_help && p.pos[0] + 1 >= kAttnHelpMinKeys;
-          if (help) aw.NS = aw.a.nsplit = 2 * p.NS < kMaxNS ? 2 * p.NS : kMaxNS;
           const int units = p.H * aw.NS;
           for (int u = blockIdx.x; u < units; u += (help ? 2 : 1) * G) {
             if constexpr (PERSIST_ATTN_WIN) attn_unit_win<HS>(aw, u, awin, lane);
@@ -781,7 +868,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
       __syncthreads();  // every slot reduced into res
       if (lane == 0) *ctr = 0u;  // next GEMV phase's slot counter (used after its staging barrier)
       TRACE(2);
-      epilogue(d, g, p, res, xres, lane, l, cs0, scr, etab);
+      epilogue<Q8>(d, g, p, res, xres, lane, l, cs0, scr, etab);
       TRACE(3);
     }
   } else {
@@ -909,6 +996,10 @@ __global__ void __launch_bounds__(PT) persistent_step_kernel(PStep p) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const unsigned tb = p.seq[0] << 12;  // tag base of this launch
+#ifndef PERSIST_CTRL_PRIO
+#define PERSIST_CTRL_PRIO 0
+#endif
+  if (wave == 0 && PERSIST_CTRL_PRIO) __builtin_amdgcn_s_setprio(PERSIST_CTRL_PRIO);
   if (wave == 0) phases<HS, true, Q8, HELP>(p, wave, lane, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, etab, tb, awin);
   else phases<HS, false, Q8, HELP>(p, wave, lane, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, etab, tb, awin);
 }

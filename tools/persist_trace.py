@@ -152,8 +152,21 @@ def main():
     live = a[:, :, 10] > a[:, :, 0]
     if live.any():
         rel = lambda k: float(np.median((a[:, :, k] - a[:, :, 0])[live]))
-        print(f"attention units ({int(live.sum() / len(att))} per layer): q {rel(8):.2f}  scores/kv {rel(9):.2f}  "
-              f"summed {rel(11):.2f}  computed {rel(10):.2f}  done {rel(3):.2f} us after phase start")
+        if args.dtype == "int8":
+            print(f"attention units ({int(live.sum() / len(att))} per layer): q {rel(8):.2f}  scores/kv {rel(9):.2f}  "
+                  f"summed {rel(11):.2f}  computed {rel(10):.2f}  done {rel(3):.2f} us after phase start")
+        else:  # attn_unit_win (fp32, batch 1): granules in, cached keys folded, computed, published
+            print(f"attention units ({int(live.sum() / len(att))} per layer): q/k/v in {rel(8):.2f}  cached keys "
+                  f"{rel(9):.2f}  computed {rel(11):.2f}  published {rel(10):.2f}  done {rel(3):.2f} us after phase start")
+        # the hand-offs around attention, per layer (median over layers): the last QKV epilogue's end,
+        # the last head published, and the Wo staging's gather, relative to the median attention start
+        qkv_end = np.stack([t[:, ph - 1, 3].max() for ph in att])
+        a0 = np.stack([np.median(t[:, ph, 0]) for ph in att])
+        pub = np.stack([(a[i, :, 10][live[i]]).max() if live[i].any() else np.nan for i in range(len(att))])
+        wo_g = np.stack([np.median(t[:, ph + 1, 8]) for ph in att])
+        print(f"around attention (median over layers, us from the median attention start): last QKV epilogue "
+              f"{np.nanmedian(qkv_end - a0):.2f}  last head published {np.nanmedian(pub - a0):.2f}  "
+              f"Wo gather (median block) {np.nanmedian(wo_g - a0):.2f}")
     # int8: repair rounds of the exact norm sums (slot 13, seqsum.hpp)
     if args.dtype == "int8":
         print("norm-sum repair rounds (mean / max over blocks and layers): " + "  ".join(
