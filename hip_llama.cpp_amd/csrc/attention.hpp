@@ -779,7 +779,23 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
     l = fmaf(l, scale, wave_sum_u(e));
 #pragma unroll
     for (int c = 0; c < VPL; ++c) o[c] *= scale;
-    for (int u = 0; u < n; ++u) {
+    // keys in order; the V reads of 8 keys are issued together (one LDS latency per 8 keys, not
+    // per key)
+    int u = 0;
+    for (; u + 8 <= n; u += 8) {
+      float vv[8][VPL];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int c = 0; c < VPL; ++c) vv[k][c] = vrows[(u + k) * vstride + lane * VPL + c];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float a = lane_f(e, u + k);
+#pragma unroll
+        for (int c = 0; c < VPL; ++c) o[c] = fmaf(a, vv[k][c], o[c]);
+      }
+    }
+    for (; u < n; ++u) {
       const float a = lane_f(e, u);
 #pragma unroll
       for (int c = 0; c < VPL; ++c) o[c] = fmaf(a, vrows[u * vstride + lane * VPL + c], o[c]);

@@ -996,10 +996,6 @@ __global__ void __launch_bounds__(PT) persistent_step_kernel(PStep p) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const unsigned tb = p.seq[0] << 12;  // tag base of this launch
-#ifndef PERSIST_CTRL_PRIO
-#define PERSIST_CTRL_PRIO 0
-#endif
-  if (wave == 0 && PERSIST_CTRL_PRIO) __builtin_amdgcn_s_setprio(PERSIST_CTRL_PRIO);
   if (wave == 0) phases<HS, true, Q8, HELP>(p, wave, lane, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, etab, tb, awin);
   else phases<HS, false, Q8, HELP>(p, wave, lane, res, xres, red, rmsw, xs, xq, xsc, sqa, scr, cwb, etab, tb, awin);
 }
