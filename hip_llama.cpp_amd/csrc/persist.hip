@@ -545,9 +545,9 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, sign
     if constexpr (Q8) {
       __syncthreads();  // the squares are in sqa
       if constexpr (ROLE0) {
-        int rounds[16] = {0};
-        const float v = d.K <= 4096 ? wave_seqsum_reg(sqa, d.K, lane, ts ? rounds : nullptr) : wave_seqsum(sqa, d.K, lane);
-        if (ts && lane == 0 && d.K <= 4096) ts[13] = (unsigned long long)rounds[0];  // (diagnostics: repair rounds)
+        int rounds = 0;  // (a register: an array here lived in scratch, zeroed on every norm)
+        const float v = d.K <= 4096 ? seqsum_reg_core<false>(sqa, d.K, lane, rounds, nullptr) : wave_seqsum(sqa, d.K, lane);
+        if (ts && lane == 0 && d.K <= 4096) ts[13] = (unsigned long long)rounds;  // (diagnostics: repair rounds)
         if (lane == 0) red[0] = v;
       }
       __syncthreads();

@@ -156,7 +156,9 @@ TL_DEVICE float reg_chain(const f4 (&r)[16], int ch4, float s) {
   return s;
 }
 
-TL_DEVICE float wave_seqsum_reg(const float* a, int n, int lane, int* rounds_out = nullptr) {
+// nrounds: the repair rounds taken (a register); fails (FAILS, diagnostics): the failing lane per round
+template <bool FAILS>
+TL_DEVICE float seqsum_reg_core(const float* a, int n, int lane, int& nrounds, int* fails) {
   const int ch = seqsum_ch(n), ch4 = ch >> 2;
   const f4* my = reinterpret_cast<const f4*>(a + lane * (ch + 4));
   f4 r[16];
@@ -188,14 +190,14 @@ TL_DEVICE float wave_seqsum_reg(const float* a, int n, int lane, int* rounds_out
     const unsigned long long bad = __ballot(lane >= lo && __float_as_uint(e) != __float_as_uint(next) &&
                                             !(e != e && next != next));
     if (!bad) {
-      if (rounds_out) *rounds_out = round + 1;
+      nrounds = round + 1;
       return total;
     }
     const int c = (int)__builtin_ctzll(bad);
     const float ec = lane_f(e, c);
-    if (rounds_out && round < 15) rounds_out[1 + round] = c;  // (diagnostics: the failing lane per round)
+    if (FAILS && round < 15) fails[round] = c;  // (diagnostics: the failing lane per round)
     if (c == 63) {
-      if (rounds_out) *rounds_out = round + 1;
+      nrounds = round + 1;
       return ec;
     }
     lo = c + 1;
@@ -203,7 +205,18 @@ TL_DEVICE float wave_seqsum_reg(const float* a, int n, int lane, int* rounds_out
     plo = lane_d(pre, lo);
     if (lane == lo) start = ec;
   }
+  nrounds = 64;
   return lane_f(e, 63);
+}
+
+// rounds_out (optional): [0] the repair rounds, [1..15] the failing lane per round (diagnostics).
+// Callers that only want the count use seqsum_reg_core<false> (no array in the caller's frame).
+TL_DEVICE float wave_seqsum_reg(const float* a, int n, int lane, int* rounds_out = nullptr) {
+  int nr = 0;
+  if (!rounds_out) return seqsum_reg_core<false>(a, n, lane, nr, nullptr);
+  const float v = seqsum_reg_core<true>(a, n, lane, nr, rounds_out + 1);
+  rounds_out[0] = nr;
+  return v;
 }
 
 // Short sums (n <= 512): the chain itself, run by every lane over the values read back from the
