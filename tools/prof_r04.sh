@@ -3,7 +3,7 @@
 # of the default bench line (B=1 fp32 persistent, plain launch: rocprofv3 crashes at exit after a
 # cooperative one), int8 B=1 and fp32 B=8; int8 B=1 FETCH_SIZE / WRITE_SIZE in separate passes.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && export TMPDIR=/tmp && rm -rf gpurun_out/prof_* gpurun_out/pmc_* && \
-B="python bench.py --skip-cpu --no-long --no-requests-point" && \
+B="python bench.py --skip-cpu --no-long --no-requests-point --no-cli-point" && \
 tools/gpujob.sh \
  "prof_b1:300:THALLAMA_PERSIST_COOP=0 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_b1 -o b1 -- $B --steps 5 --prof-steps 4" \
  "prof_int8:300:THALLAMA_PERSIST_COOP=0 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_int8 -o i8 -- $B --dtype int8 --steps 5 --prof-steps 4" \
