@@ -149,9 +149,11 @@ def main():
     # done (us after the phase start)
     att = [ph for ph in range(1, nph - 1, 5)]
     a = np.stack([t[:, ph, :] for ph in att])  # [layers][G][slots]
-    live = a[:, :, 10] > a[:, :, 0]
+    # live: blocks whose unit stamped its granules in (fp32) / its publish (int8); a unit that is
+    # not its head's last split publishes nothing (slot 10 stays from an earlier phase)
+    live = (a[:, :, 8] > a[:, :, 0]) if args.dtype == "f32" else (a[:, :, 10] > a[:, :, 0])
     if live.any():
-        rel = lambda k: float(np.median((a[:, :, k] - a[:, :, 0])[live]))
+        rel = lambda k: float(np.median((a[:, :, k] - a[:, :, 0])[live & (a[:, :, k] > a[:, :, 0])]))
         if args.dtype == "int8":
             print(f"attention units ({int(live.sum() / len(att))} per layer): q {rel(8):.2f}  scores/kv {rel(9):.2f}  "
                   f"summed {rel(11):.2f}  computed {rel(10):.2f}  done {rel(3):.2f} us after phase start")
@@ -162,7 +164,8 @@ def main():
         # the last head published, and the Wo staging's gather, relative to the median attention start
         qkv_end = np.stack([t[:, ph - 1, 3].max() for ph in att])
         a0 = np.stack([np.median(t[:, ph, 0]) for ph in att])
-        pub = np.stack([(a[i, :, 10][live[i]]).max() if live[i].any() else np.nan for i in range(len(att))])
+        pubm = a[:, :, 10] > a[:, :, 0]  # blocks whose unit published a head in this phase
+        pub = np.stack([(a[i, :, 10][pubm[i]]).max() if pubm[i].any() else np.nan for i in range(len(att))])
         wo_g = np.stack([np.median(t[:, ph + 1, 8]) for ph in att])
         print(f"around attention (median over layers, us from the median attention start): last QKV epilogue "
               f"{np.nanmedian(qkv_end - a0):.2f}  last head published {np.nanmedian(pub - a0):.2f}  "
