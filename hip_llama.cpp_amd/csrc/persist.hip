@@ -72,9 +72,6 @@ constexpr unsigned kSpinLimit = 1u << 18;
 // The helper lives in its own kernel instantiation (HELP), launched only at such positions: its
 // registers (the streaming wave's slots stay live across the unit) spill 20 B in the shared
 // code, which cost the short-context step 1.2% (profiles/r04/attn_help_ab.txt).
-#ifndef PERSIST_ATTN_HELP
-#define PERSIST_ATTN_HELP 1
-#endif
 #ifndef PERSIST_XCD_SKEW
 #define PERSIST_XCD_SKEW 4
 #endif
@@ -1012,7 +1009,7 @@ template <int HS, bool Q8, bool HELP = false>
 static const void* kfn() { return (const void*)persistent_step_kernel<HS, Q8, HELP>; }
 static const void* kernel_of(const PStep& p) {
   if (p.q8) return p.hs == 128 ? kfn<128, true>() : kfn<64, true>();
-  if (PERSIST_ATTN_HELP && p.attn_help && p.long_ctx) return p.hs == 128 ? kfn<128, false, true>() : kfn<64, false, true>();
+  if (p.attn_help && p.long_ctx) return p.hs == 128 ? kfn<128, false, true>() : kfn<64, false, true>();
   return p.hs == 128 ? kfn<128, false>() : kfn<64, false>();
 }
 
@@ -1087,7 +1084,7 @@ bool persistent_prepare(PStep& p, int ncu, const char** why) {
   }
   if (lds_bytes(p) > kDynLdsCap) return fail("activations do not fit the LDS");
   p.attn_help = 0;
-  if (!p.q8 && PERSIST_ATTN_WIN && PERSIST_ATTN_HELP && p.NS * 2 <= kMaxNS) {  // room for a second attention window in the strip?
+  if (!p.q8 && PERSIST_ATTN_WIN && p.NS * 2 <= kMaxNS) {  // room for a second attention window in the strip?
     const int base = p.pad_floats, need = attn_win_floats(p.hs);
     if (base < need) p.pad_floats = need;
     if (lds_bytes(p) <= kDynLdsCap) p.attn_help = 1;
