@@ -195,6 +195,19 @@ def plumbing(args, world, rank):
 
 
 # ---------------------------------------------------------------- --workload cli (configs[4])
+def cli_passes(stdout):
+    """(tokens, seconds) of each pass the CLI served: its "pass i: tokens N seconds S" lines
+    (app/run.cpp, THALLAMA_PASSES), or, for one pass, the reference's own summary lines
+    ("Total achieved token: N", "elapsed time(s): S, ...", src/llama.cpp:1062-1070)."""
+    lines = stdout.splitlines()
+    runs = [(int(ln.split()[3]), float(ln.split()[5])) for ln in lines if ln.startswith("pass ")]
+    if not runs:
+        tot = [ln for ln in lines if ln.startswith("Total achieved token:")]
+        el = [ln for ln in lines if ln.startswith("elapsed time(s):")]
+        runs = [(int(tot[-1].split()[-1]), float(el[-1].split()[2].rstrip(",")))]
+    return runs
+
+
 def cli_serve(args, world, B, passes, warmup):
     """One run of the drop-in CLI (build/apps/llama, app/run.cpp — the reference's
     test_data_parallelism, src/llama.cpp:891-1083: one host thread per GPU, B slots per thread, one
@@ -236,11 +249,7 @@ def cli_serve(args, world, B, passes, warmup):
     if p.returncode != 0:
         log(p.stdout[-4000:], p.stderr[-4000:])
         raise SystemExit(f"bench.py: the CLI failed ({p.returncode})")
-    runs = [(int(ln.split()[3]), float(ln.split()[5])) for ln in p.stdout.splitlines() if ln.startswith("pass ")]
-    if not runs:  # one pass: the reference's own summary lines
-        tot = [ln for ln in p.stdout.splitlines() if ln.startswith("Total achieved token:")]
-        el = [ln for ln in p.stdout.splitlines() if ln.startswith("elapsed time(s):")]
-        runs = [(int(tot[-1].split()[-1]), float(el[-1].split()[2].rstrip(",")))]
+    runs = cli_passes(p.stdout)
     timed_p = runs[warmup:] or runs
     tokens = sum(t for t, _ in timed_p)
     secs = sum(x for _, x in timed_p)
