@@ -56,7 +56,7 @@ constexpr int PW = NBUF == 2 ? 9 : 8;  // waves per block: 1 control + PW-1 stre
 constexpr int PT = PW * 64;  // threads per block
 constexpr int PL = 8;        // wave-loads per slot (8 KiB per wave)
 constexpr int NSW = PW - 1;  // streaming waves per block
-constexpr int SB = 4;        // staged float4 per thread and batch (granule loads in flight)
+constexpr int SB = 2;        // staged float4 per thread and batch (granule loads in flight; profiles/r04/persist_knobs_ab.txt)
 constexpr int kPResidFloats = 256;  // residual-stream slice per block (LDS)
 constexpr unsigned kSpinLimit = 1u << 18;
 #ifndef PERSIST_ATTN_CH
