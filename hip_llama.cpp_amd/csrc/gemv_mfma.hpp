@@ -28,13 +28,11 @@ namespace tl {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-#ifndef MFMA_WAVES
-#define MFMA_WAVES 4
-#endif
-#ifndef MFMA_U
-#define MFMA_U 4
-#endif
-constexpr int kMfmaWaves = MFMA_WAVES;
+// 4 waves per block (the norm and epilogue maps assume 256 threads) and 4 16-k steps per group
+// (256-B row runs; 8 steps = 512-B runs needed 226-254 VGPRs, one wave per SIMD, and lost 12% at
+// batch 8: profiles/r04/mfma_u8_ab.txt)
+constexpr int kMfmaWaves = 4;
+constexpr int kMfmaU = 4;
 
 // One output of the decode epilogues (gemv.hpp epilogue) for row/item `item`, sequence b.
 template <int MODE>
@@ -119,7 +117,7 @@ __global__ void __launch_bounds__(kMfmaWaves * 64) gemv_mfma_kernel(GemvParams p
   constexpr int W = kMfmaWaves;
   constexpr bool TWO = MODE == GM_SWIGLU;
   constexpr int NR = TWO ? 2 : 1;      // weight tiles per group; tile NR is the activations
-  constexpr int U = MFMA_U;            // 16-k steps per group
+  constexpr int U = kMfmaU;            // 16-k steps per group
   constexpr int LPR = U * 4;           // lanes per row in a load (16 B each): 256-B runs
   constexpr int RPI = 64 / LPR;        // rows per load instruction
   constexpr int NI = 16 / RPI;         // load instructions per 16-row tile
