@@ -29,8 +29,9 @@ namespace tl {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // 4 waves per block (the norm and epilogue maps assume 256 threads) and 4 16-k steps per group
-// (256-B row runs; 8 steps = 512-B runs needed 226-254 VGPRs, one wave per SIMD, and lost 12% at
-// batch 8: profiles/r04/mfma_u8_ab.txt)
+// (256-B row runs, four rows per load instruction, which the launcher's XI counts assume; 8 steps =
+// 512-B runs needed 226-254 VGPRs, one wave per SIMD, and lost 12% at batch 8:
+// profiles/r04/mfma_u8_ab.txt)
 constexpr int kMfmaWaves = 4;
 constexpr int kMfmaU = 4;
 
