@@ -34,9 +34,11 @@ and RCCL-broadcasts them; no collective on the data path (weak scaling).
                     [--model 7b|110m] [--dtype f32|int8] [--batch B]
 """
 import argparse
+import atexit
 import hashlib
 import json
 import os
+import shutil
 import socket
 import subprocess
 import sys
@@ -58,10 +60,76 @@ PROMPTS = os.path.join(GOLDEN, "gen_in_64.txt")  # the reference's assets/in/gen
 TOKENIZER = os.path.join(GOLDEN, "tokenizer.bin")  # the reference's assets/tokenizer.bin
 
 
-def fixture_path(mname, dtype, B):
-    """The committed output file of the request job at B slots per GPU (one process, one GPU,
-    all 64 prompts; bench.py --workload requests --batch B --write-fixture)."""
-    return os.path.join(GOLDEN, f"bench_requests_{mname}_{dtype}_greedy{'' if B == 8 else f'_b{B}'}.json")
+def fixture_path(mname, dtype, T):
+    """The expected output file of the request job (prompts of gen_in_64.txt, greedy, each request to
+    position T - 1 or BOS/EOS), made by the pinned CPU path: tests/golden/make_golden_requests.py
+    (oracle/oracle.c, bit-identical to the reference's src/seq.cpp).  Requests are independent, so
+    one file serves every slot count.  None where no such fixture exists."""
+    p = os.path.join(GOLDEN, f"requests_{mname}_{dtype}_gen_in_64.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        fx = json.load(f)
+    return p if fx.get("decode_len") == T and fx.get("seed") == SEED else None
+
+
+def compare_request_file(got, fx, n, tie_margin=1e-4):
+    """The CLI's output file for the first n requests against the fixture.  Byte-identical, or else
+    every request's record equals the fixture's except a request whose greedy decode reaches a
+    near-tie of the CPU reference (top-2 logit margin < tie_margin: fp32 summation order alone can
+    flip it) and leaves the fixture's text within that step's piece; the rest of such a request is
+    unpinned.  Returns {"identical", "diverged": [[request, position, margin]], "unexplained": [...],
+    "ok"}; ok allows at most as many diverged requests as the fixture has requests with a tie under
+    1e-5 (tests/test_requests_gpu.py, the same rule as tests/test_cli_gpu.py)."""
+    ws = [o.encode("latin-1") + b"\n" for o in fx["outputs"][:n]]  # a record: output + "\n"
+    head = f"{n}\n".encode()
+    res = {"identical": got == head + b"".join(ws), "requests": n, "diverged": [], "unexplained": []}
+    if not res["identical"]:
+        if not got.startswith(head):
+            res["unexplained"].append("header")
+            rest = b""
+        else:
+            rest = got[len(head):]
+        for i, w in enumerate(ws):
+            if not rest:
+                res["unexplained"].append(f"record {i} missing")
+                break
+            if rest.startswith(w):
+                rest = rest[len(w):]
+                continue
+            first = next((k for k, (a, b) in enumerate(zip(rest, w)) if a != b), min(len(rest), len(w)))
+            ties = [t for t in fx["near_ties"][i] if t[1] < tie_margin and t[2] <= first]
+            if ties and first - ties[-1][2] <= 64:
+                res["diverged"].append([i, ties[-1][0], ties[-1][1]])
+            else:
+                res["unexplained"].append(i)
+            if i + 1 < n:  # the next record starts with its prompt (forced tokens: never diverges)
+                k = rest.find(b"\n\n" + ws[i + 1][:48])
+                if k < 0:
+                    res["unexplained"].append(f"record {i + 1} not found")
+                    rest = b""
+                    break
+                rest = rest[k + 2:]
+            else:
+                rest = b""
+        if rest:
+            res["unexplained"].append("trailing bytes")
+    n_tight = sum(1 for ts in fx["near_ties"][:n] if any(t[1] < 1e-5 for t in ts))
+    res["ok"] = res["identical"] or (not res["unexplained"] and len(res["diverged"]) <= n_tight)
+    return res
+
+
+_WORKDIRS = []
+
+
+def workdir(prefix):
+    """A scratch directory under the repository (visible to every rank); removed at exit whatever
+    happens to the run (atexit also runs on SystemExit and uncaught exceptions)."""
+    d = tempfile.mkdtemp(prefix=prefix, dir=REPO)
+    if not _WORKDIRS:
+        atexit.register(lambda: [shutil.rmtree(x, ignore_errors=True) for x in _WORKDIRS])
+    _WORKDIRS.append(d)
+    return d
 
 
 def log(*a):
@@ -93,23 +161,22 @@ def parse_args(argv):
     ap.add_argument("--no-cli-point", action="store_true", help="skip the 1-GPU CLI runs (-b 1 and -b 8)")
     ap.add_argument("--host-argmax", action="store_true",
                     help="requests: greedy sampling on the host from copied logits (the reference's way)")
-    ap.add_argument("--write-fixture", action="store_true",
-                    help="requests: serve all 64 prompts in this process and write the output fixture")
     ap.add_argument("--cpu-baseline-tokens", type=int, default=0,
                     help="greedy tokens the CPU baseline decodes (0: as many as fit --cpu-baseline-seconds)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-aggregate", type=int, default=1 << 20,
                     help="max decoders of the aggregate CPU baseline (default: the host CPU share)")
     ap.add_argument("--skip-cpu", action="store_true")
-    ap.add_argument("--prof-steps", type=int, default=16)
+    ap.add_argument("--prof-steps", type=int, default=0,
+                    help="positions the roofline object's HIP events cover (0: all decode-len, the headline's span)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (CPU rehearsal)")
     ap.add_argument("--device-map", default="", help="comma list: local rank -> HIP device (rehearsals that "
                                                      "put several ranks on one GPU)")
     ap.add_argument("--plumbing", action="store_true",
                     help="no GPU: ranks, sharding and output gathering over a deterministic CPU step (tests)")
     args = ap.parse_args(argv)
-    if args.prof_steps < 1:
-        ap.error("--prof-steps must be >= 1 (the roofline object times the dominant kernel over them)")
+    if args.prof_steps < 0:
+        ap.error("--prof-steps must be >= 0 (0: the whole decode, the headline's span)")
     if args.gpus < 1 or args.steps < 1 or args.warmup < 0:
         ap.error("--gpus and --steps must be >= 1, --warmup >= 0")
     return args
@@ -168,7 +235,7 @@ def plumbing(args, world, rank):
             lg[b, (int(t) * 7919 + int(p) * 104729 + 13) % (V - 3) + 3] = 1.0
         return lg
     n = args.prompts_per_gpu * world
-    wd = tempfile.mkdtemp(prefix=".bench_", dir=REPO)
+    wd = workdir(".bench_")
     req = write_requests(read_prompts(PROMPTS, n), wd) if rank == 0 else None
     if world > 1:
         box = [req]
@@ -200,7 +267,8 @@ def cli_passes(stdout):
     (app/run.cpp, THALLAMA_PASSES), or, for one pass, the reference's own summary lines
     ("Total achieved token: N", "elapsed time(s): S, ...", src/llama.cpp:1062-1070)."""
     lines = stdout.splitlines()
-    runs = [(int(ln.split()[3]), float(ln.split()[5])) for ln in lines if ln.startswith("pass ")]
+    runs = [(int(ln.split()[3]), float(ln.split()[5])) for ln in lines
+            if ln.startswith("pass ") and ln.split()[1].endswith(":")]
     if not runs:
         tot = [ln for ln in lines if ln.startswith("Total achieved token:")]
         el = [ln for ln in lines if ln.startswith("elapsed time(s):")]
@@ -230,7 +298,7 @@ def cli_serve(args, world, B, passes, warmup):
     dims = list(cfg_t)
     dims[5] = dims[5] if shared else -dims[5]
     spec = "synth:" + ",".join(str(v) for v in dims) + f":{SEED}" + (f":q8:{args.group_size}" if q8 else "")
-    wd = tempfile.mkdtemp(prefix=".bench_cli_", dir=REPO)
+    wd = workdir(".bench_cli_")
     req = write_requests(read_prompts(PROMPTS, n), wd)
     out = os.path.join(wd, "out.txt")
     env = dict(os.environ)
@@ -256,14 +324,35 @@ def cli_serve(args, world, B, passes, warmup):
     load = next((float(ln.split()[-1]) for ln in p.stdout.splitlines() if ln.startswith("Load model time")), None)
     with open(out, "rb") as f:
         got = f.read()
-    fx_path = fixture_path(mname, args.dtype, B)
-    match = None
-    if os.path.exists(fx_path):
+    fx_path = fixture_path(mname, args.dtype, T)
+    check = None
+    if fx_path:
         with open(fx_path) as f:
             fx = json.load(f)
-        if fx.get("decode_len") == T and fx.get("seed") == SEED and len(fx["outputs"]) >= n:
-            want = f"{n}\n".encode() + b"".join(o.encode("utf-8", "surrogateescape") + b"\n" for o in fx["outputs"][:n])
-            match = got == want
+        if len(fx["outputs"]) >= n:
+            check = compare_request_file(got, fx, n)
+            check["tokens_equal_fixture"] = tokens == (sum(fx["achieved_tokens"][:n]) * len(timed_p))
+    # per pass, per GPU (worker): tokens, requests, seconds from the pass start to its last step
+    per_gpu = {}
+    for ln in p.stdout.splitlines():
+        f_ = ln.replace(":", "").split()
+        if ln.startswith("pass ") and len(f_) >= 11 and f_[2] == "worker":
+            per_gpu.setdefault(int(f_[1]), []).append({"worker": int(f_[3]), "device": int(f_[5]),
+                                                       "tokens": int(f_[7]), "requests": int(f_[9]),
+                                                       "seconds": float(f_[11])})
+    timed_ids = sorted(per_gpu)[warmup:] or sorted(per_gpu)
+    gpus = []
+    for w in sorted({g["worker"] for i in timed_ids for g in per_gpu[i]}):
+        rows = [g for i in timed_ids for g in per_gpu[i] if g["worker"] == w]
+        tk, sc = sum(g["tokens"] for g in rows), sum(g["seconds"] for g in rows)
+        gpus.append({"worker": w, "device": rows[0]["device"], "tokens_per_pass": rows[0]["tokens"],
+                     "requests_per_pass": rows[0]["requests"], "seconds_per_pass": round(sc / len(rows), 4),
+                     "tok_s": round(tk / sc, 2) if sc > 0 else None})
+    rep = next((ln.split() for ln in p.stdout.splitlines() if ln.startswith("replication: ") and " to " in ln), None)
+    replication = ({"path": rep[1], "replicas": int(rep[3]), "gpus": int(rep[6].lstrip("(")),
+                    "seconds": float(rep[-2])} if rep else None)
+    fallbacks = [ln for ln in p.stdout.splitlines() if ln.startswith("replication: ") and "falling back" in ln]
+    cpus = [ln for ln in p.stdout.splitlines() if ln.startswith("worker ") and " cpu " in ln]
     for f_ in (req, out):
         os.remove(f_)
     os.rmdir(wd)
@@ -272,9 +361,12 @@ def cli_serve(args, world, B, passes, warmup):
             "cmd": " ".join(os.path.relpath(c, REPO) if c.startswith(REPO) else c for c in cmd),
             "passes": [{"tokens": t, "seconds": x} for t, x in runs], "warmup_passes": warmup,
             "load_s": load, "wall_s": round(wall, 2), "replicas": args.cli_replicas or world,
-            "output_matches_fixture": match,
-            "fixture": os.path.relpath(fx_path, REPO) if os.path.exists(fx_path) else None,
-            "output_sha": hashlib.sha256(got).hexdigest()[:16]}
+            "output_matches_fixture": check["identical"] if check else None,
+            "fixture_check": check,
+            "fixture": os.path.relpath(fx_path, REPO) if fx_path else None,
+            "output_sha": hashlib.sha256(got).hexdigest()[:16],
+            "replication": replication, "replication_fallbacks": fallbacks, "worker_cpus": cpus,
+            "per_gpu": gpus}
 
 
 def cli_run(args, world, rank):
@@ -446,7 +538,7 @@ def main(argv=None):
         """Per-kernel-class HIP events on the decoder's stream over an eager replay of the first
         prof-steps positions; the dominant kernel's roofline object."""
         prof, prof_ml = {}, {}
-        P = min(args.prof_steps, T)
+        P = min(args.prof_steps or T, T)
         persistent = dec.persistent()
         step_bytes_p = sum(launch_bytes(B, tl.K_STEP, [p] * B) for p in range(P)) / P
 
@@ -515,12 +607,12 @@ def main(argv=None):
         return roof, rnd(prof), rnd(prof_ml)
 
     # ------------------------------------------------------------ request workload (configs[4])
-    def requests_run(dec, B, n_per_rank, passes, warm, fixture_write=False):
+    def requests_run(dec, B, n_per_rank, passes, warm):
         """The reference test mode over gen_in_64.txt: n_per_rank prompts per rank, B slots, greedy,
         each request to position T-1 or EOS/BOS.  Returns the measurement dict (rank 0)."""
         from hip_llama_cpp_amd import host as H
         n = n_per_rank * world
-        wd = tempfile.mkdtemp(prefix=".bench_", dir=REPO) if rank == 0 else None
+        wd = workdir(".bench_") if rank == 0 else None
         prompts = read_prompts(PROMPTS, n)
         req = write_requests(prompts, wd) if rank == 0 else None
         if world > 1:
@@ -547,22 +639,14 @@ def main(argv=None):
         el = timed(one, passes)
         res = None
         if rank == 0:
-            outs = [o.decode("utf-8", "replace") for o in outs]
-            fx_path = fixture_path(mname, args.dtype, B)
-            match, fx_n = None, 0
-            if fixture_write:
-                with open(fx_path, "w") as f:
-                    json.dump({"generator": "bench.py --write-fixture (one process, one GPU, "
-                                            f"{B} slots over all {n} prompts)",
-                               "model": mname, "dtype": args.dtype, "seed": SEED, "decode_len": T,
-                               "prompts": "tests/golden/gen_in_64.txt (reference assets/in/gen_in_64.txt)",
-                               "outputs": outs}, f, indent=0)
-            if os.path.exists(fx_path):
+            fx_path = fixture_path(mname, args.dtype, T)
+            check = None
+            if fx_path:
                 with open(fx_path) as f:
                     fx = json.load(f)
-                if fx.get("decode_len") == T and fx.get("seed") == SEED:
-                    fx_n = min(len(outs), len(fx["outputs"]))
-                    match = outs[:fx_n] == fx["outputs"][:fx_n]
+                if len(fx["outputs"]) >= n:
+                    got = f"{n}\n".encode() + b"".join(o + b"\n" for o in outs)
+                    check = compare_request_file(got, fx, n)
             tok_s = gen[0] * passes / el
             dec_tokens = gen[0] - prompt_pos
             per_rank_roof = HBM_PEAK_GBS * 1e9 / token_bytes(B, (T - 1) / 2.0) * B
@@ -575,8 +659,9 @@ def main(argv=None):
                    "prompt_positions_per_pass": prompt_pos,
                    "roofline_decode_tok_s_per_gpu": round(per_rank_roof, 1),
                    "frac_of_roofline": round(dec_tokens * passes / el / world / per_rank_roof, 4),
-                   "outputs_sha": sha(outs), "output_matches_fixture": match, "fixture_requests_compared": fx_n,
-                   "fixture": os.path.relpath(fx_path, REPO) if os.path.exists(fx_path) else None}
+                   "outputs_sha": sha([o.decode("latin-1") for o in outs]),
+                   "output_matches_fixture": check["identical"] if check else None, "fixture_check": check,
+                   "fixture": os.path.relpath(fx_path, REPO) if fx_path else None}
             os.remove(out)
             os.remove(req)
             os.rmdir(wd)
@@ -590,10 +675,10 @@ def main(argv=None):
         state, dec = make_decoder(B)
         log(f"[rank {rank}] {mname} {args.dtype} requests B={B} init {t_init:.2f}s (broadcast {t_bcast:.2f}s) "
             f"path {'persistent' if dec.persistent() else 'multi-launch'}")
-        per = 64 if args.write_fixture else args.prompts_per_gpu
+        per = args.prompts_per_gpu
         if per * world > 64:
             raise SystemExit(f"{per} prompts per GPU x {world} GPUs > the 64 prompts of gen_in_64.txt")
-        r = requests_run(dec, B, per, args.steps, args.warmup, fixture_write=args.write_fixture and world == 1)
+        r = requests_run(dec, B, per, args.steps, args.warmup)
         roof, prof, prof_ml = profile_roofline(dec, B) if rank == 0 else (None, {}, {})
         if rank == 0:
             out = {"metric": "decode tokens/sec (greedy, whole model) + achieved HBM GB/s fraction",
@@ -678,6 +763,8 @@ def main(argv=None):
                 pass
 
         roof, prof, prof_ml = profile_roofline(dec, B) if rank == 0 else (None, {}, {})
+        if roof:  # the same bytes over the timed region's own clock (graph replays, launch gaps included)
+            roof["frac_timed_region"] = round(step_gbs / HBM_PEAK_GBS, 4)
 
         # the 1-GPU point of the request workload (configs[4]'s per-GPU share), so the N > 1 lines
         # have their own single-GPU reference

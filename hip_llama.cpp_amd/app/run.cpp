@@ -20,6 +20,9 @@
 #include <string.h>
 #include <time.h>
 
+#include <ctype.h>
+#include <sched.h>
+
 #include <string>
 #include <vector>
 
@@ -36,15 +39,6 @@
       exit(EXIT_FAILURE);                                                                        \
     }                                                                                            \
   } while (0)
-#define NCCL_OK(cmd)                                                                             \
-  do {                                                                                           \
-    ncclResult_t r_ = (cmd);                                                                     \
-    if (r_ != ncclSuccess) {                                                                     \
-      fprintf(stderr, "RCCL error %s at %s:%d\n", ncclGetErrorString(r_), __FILE__, __LINE__);  \
-      exit(EXIT_FAILURE);                                                                        \
-    }                                                                                            \
-  } while (0)
-
 static long time_in_ms() {
   struct timespec ts;
   clock_gettime(CLOCK_REALTIME, &ts);
@@ -197,9 +191,11 @@ static void synth_on_device(const ModelFile& m, void* arena) {
   HIP_OK(hipDeviceSynchronize());
 }
 
-// One GPU's replica: the weight arena, run state for `batch` sequences, the decoder.
+// One GPU's replica: the weight arena, run state for `batch` sequences, the decoder, and the host
+// core its worker thread is pinned to.
 struct Replica {
   int dev = 0;
+  int cpu = -1;
   void* arena = nullptr;
   TransformerWeights w{};
   Q8TransformerWeights w8{};
@@ -208,11 +204,173 @@ struct Replica {
   thallama_decoder* dec = nullptr;
 };
 
-// Weights on every device: one H2D copy to device 0, then an RCCL broadcast (in 1 GiB
-// pieces) into every other device's arena.  n_rep > n_dev (THALLAMA_REPLICAS, a rehearsal of the
-// multi-GPU worker split on fewer GPUs): replica r lives on device r % n_dev and the replicas
-// past the first n_dev get their weights by a device-to-device copy.
-static std::vector<Replica> replicate(ModelFile& m, int n_dev, int n_rep, int batch) {
+static double now_s() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+// How the weight image reached replicas 1..n-1 (printed, and parsed by bench.py).
+enum class RepPath { none, rccl, peer, upload };
+static const char* rep_name(RepPath p) {
+  return p == RepPath::rccl ? "rccl" : p == RepPath::peer ? "peer" : p == RepPath::upload ? "upload" : "none";
+}
+
+// RCCL broadcast of replica 0's arena into replicas 1..k-1 (device of replica i = reps[i].dev), in
+// 1 GiB pieces, one communicator per replica.  Every call is checked and the transfer is polled
+// against a deadline, so a failed or stalled RCCL returns an error (communicators aborted) instead
+// of ending the process: the caller then replicates another way.
+static std::string rccl_broadcast(std::vector<Replica>& reps, int k, size_t bytes) {
+  std::vector<ncclComm_t> comms((size_t)k, nullptr);
+  std::vector<int> devs((size_t)k);
+  for (int d = 0; d < k; ++d) devs[d] = reps[d].dev;
+  ncclResult_t nr = ncclCommInitAll(comms.data(), k, devs.data());
+  if (nr != ncclSuccess) return std::string("ncclCommInitAll: ") + ncclGetErrorString(nr);
+  std::string err;
+  std::vector<hipStream_t> st((size_t)k, nullptr);
+  for (int d = 0; d < k && err.empty(); ++d) {
+    if (hipSetDevice(reps[d].dev) != hipSuccess || hipStreamCreateWithFlags(&st[d], hipStreamNonBlocking) != hipSuccess)
+      err = "stream creation on device " + std::to_string(reps[d].dev);
+  }
+  const size_t piece = (size_t)1 << 30;
+  for (size_t off = 0; off < bytes && err.empty(); off += piece) {
+    const size_t cnt = bytes - off < piece ? bytes - off : piece;
+    nr = ncclGroupStart();
+    for (int d = 0; d < k && nr == ncclSuccess; ++d)
+      nr = ncclBroadcast((char*)reps[0].arena + off, (char*)reps[d].arena + off, cnt, ncclChar, 0, comms[d], st[d]);
+    const ncclResult_t ne = ncclGroupEnd();
+    if (nr != ncclSuccess || ne != ncclSuccess)
+      err = std::string("ncclBroadcast: ") + ncclGetErrorString(nr != ncclSuccess ? nr : ne);
+  }
+  // poll to completion: ~0.1 s per GiB over xGMI; allow 60 s + 1 s per GiB before giving up
+  const double deadline = now_s() + 60.0 + (double)bytes / (1 << 30);
+  for (int d = 0; d < k && err.empty(); ++d) {
+    (void)hipSetDevice(reps[d].dev);
+    hipError_t q;
+    while ((q = hipStreamQuery(st[d])) == hipErrorNotReady) {
+      ncclResult_t async = ncclSuccess;
+      ncclCommGetAsyncError(comms[d], &async);
+      if (async != ncclSuccess) {
+        err = std::string("RCCL async error: ") + ncclGetErrorString(async);
+        break;
+      }
+      if (now_s() > deadline) {
+        err = "RCCL broadcast did not complete before the deadline";
+        break;
+      }
+      struct timespec ts = {0, 1000000};
+      nanosleep(&ts, nullptr);
+    }
+    if (err.empty() && q != hipSuccess) err = std::string("broadcast stream: ") + hipGetErrorString(q);
+  }
+  for (int d = 0; d < k; ++d) {
+    if (comms[d]) {
+      if (err.empty()) ncclCommDestroy(comms[d]);
+      else ncclCommAbort(comms[d]);
+    }
+  }
+  for (int d = 0; d < k; ++d) {
+    if (!st[d]) continue;
+    (void)hipSetDevice(reps[d].dev);
+    if (err.empty()) (void)hipStreamSynchronize(st[d]);
+    (void)hipStreamDestroy(st[d]);
+  }
+  (void)hipSetDevice(0);
+  return err;
+}
+
+// Device-to-device copies from replica 0 (hipMemcpyPeerAsync: over xGMI between GPUs, a local copy
+// when the replica shares GPU 0) into replicas [from, n).
+static std::string peer_copies(std::vector<Replica>& reps, int from, size_t bytes) {
+  for (size_t d = (size_t)from; d < reps.size(); ++d) {
+    Replica& r = reps[d];
+    hipStream_t st = nullptr;
+    if (hipSetDevice(r.dev) != hipSuccess || hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess)
+      return "stream creation on device " + std::to_string(r.dev);
+    hipError_t e = hipMemcpyPeerAsync(r.arena, r.dev, reps[0].arena, reps[0].dev, bytes, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+    if (e != hipSuccess) return std::string("hipMemcpyPeer to device ") + std::to_string(r.dev) + ": " + hipGetErrorString(e);
+  }
+  (void)hipSetDevice(0);
+  return "";
+}
+
+// The reference's way (src/models.cpp:86-125 once per GPU thread): each replica from the host image,
+// or, for a synthetic model, the generator run again on the replica's device.
+static void upload_each(ModelFile& m, std::vector<Replica>& reps, int from) {
+  for (size_t d = (size_t)from; d < reps.size(); ++d) {
+    HIP_OK(hipSetDevice(reps[d].dev));
+    if (m.payload) HIP_OK(hipMemcpy(reps[d].arena, m.payload, m.bytes, hipMemcpyHostToDevice));
+    else synth_on_device(m, reps[d].arena);
+  }
+  HIP_OK(hipSetDevice(0));
+}
+
+// The host cores next to a device: its PCI function's local_cpulist, intersected with this process's
+// affinity mask (empty when sysfs does not say).
+static std::vector<int> local_cpus(int dev, const cpu_set_t& allowed) {
+  std::vector<int> out;
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, dev) != hipSuccess) return out;
+  for (char* c = bus; *c; ++c) *c = (char)tolower(*c);
+  const std::string path = std::string("/sys/bus/pci/devices/") + bus + "/local_cpulist";
+  FILE* f = fopen(path.c_str(), "r");
+  if (!f) return out;
+  char line[4096] = {0};
+  const bool got = fgets(line, sizeof line, f) != nullptr;
+  fclose(f);
+  if (!got) return out;
+  for (char* tok = strtok(line, ",\n"); tok; tok = strtok(nullptr, ",\n")) {
+    int a = 0, b = 0;
+    const int n = sscanf(tok, "%d-%d", &a, &b);
+    if (n < 1) continue;
+    if (n == 1) b = a;
+    for (int c = a; c <= b && c < CPU_SETSIZE; ++c)
+      if (CPU_ISSET(c, &allowed)) out.push_back(c);
+  }
+  return out;
+}
+
+// Worker w's core (the reference pins thread gid to core gid, src/llama.cpp:922-925): the next unused
+// core local to its GPU, else the next unused core this process may run on.
+static void assign_cpus(std::vector<Replica>& reps) {
+  cpu_set_t allowed;
+  CPU_ZERO(&allowed);
+  if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return;
+  std::vector<int> all;
+  for (int c = 0; c < CPU_SETSIZE; ++c)
+    if (CPU_ISSET(c, &allowed)) all.push_back(c);
+  if (all.empty()) return;
+  std::vector<char> used((size_t)CPU_SETSIZE, 0);
+  for (auto& r : reps) {
+    for (int c : local_cpus(r.dev, allowed))
+      if (!used[c]) {
+        r.cpu = c;
+        break;
+      }
+    if (r.cpu < 0)
+      for (int c : all)
+        if (!used[c]) {
+          r.cpu = c;
+          break;
+        }
+    if (r.cpu < 0) r.cpu = all[(size_t)(&r - reps.data()) % all.size()];
+    used[r.cpu] = 1;
+  }
+}
+
+// Weights on every replica: one H2D copy (or on-device synthesis) into replica 0, then replicas
+// 1..n-1 by, in order of preference:
+//   rccl   — ncclBroadcast over xGMI from GPU 0 (one replica per GPU);
+//   peer   — hipMemcpyPeer from GPU 0 (also how replicas that share a GPU are filled);
+//   upload — every replica from the host image / the generator, as the reference does.
+// A failing path falls through to the next, reported, instead of ending the run.
+// THALLAMA_REPLICATE=rccl|peer|upload picks the first path tried (tests: forced RCCL over replicas
+// that share one GPU fails in ncclCommInitAll and exercises the fall-through).  n_rep > n_dev
+// (THALLAMA_REPLICAS, a rehearsal of the multi-GPU worker split on fewer GPUs): replica r lives on
+// device r % n_dev.
+static std::vector<Replica> replicate(ModelFile& m, int n_dev, int n_rep, int batch, RepPath* used, double* rep_s) {
   std::vector<Replica> reps((size_t)n_rep);
   for (int d = 0; d < n_rep; ++d) {
     reps[d].dev = d % n_dev;
@@ -222,36 +380,40 @@ static std::vector<Replica> replicate(ModelFile& m, int n_dev, int n_rep, int ba
   HIP_OK(hipSetDevice(0));
   if (m.payload) HIP_OK(hipMemcpy(reps[0].arena, m.payload, m.bytes, hipMemcpyHostToDevice));
   else synth_on_device(m, reps[0].arena);
-  if (n_dev > 1) {
-    std::vector<ncclComm_t> comms((size_t)n_dev);
-    std::vector<int> devs((size_t)n_dev);
-    for (int d = 0; d < n_dev; ++d) devs[d] = d;
-    NCCL_OK(ncclCommInitAll(comms.data(), n_dev, devs.data()));
-    std::vector<hipStream_t> st((size_t)n_dev);
-    for (int d = 0; d < n_dev; ++d) {
-      HIP_OK(hipSetDevice(d));
-      HIP_OK(hipStreamCreate(&st[d]));
-    }
-    const size_t piece = (size_t)1 << 30;  // bytes
-    for (size_t off = 0; off < m.bytes; off += piece) {
-      const size_t cnt = m.bytes - off < piece ? m.bytes - off : piece;
-      NCCL_OK(ncclGroupStart());
-      for (int d = 0; d < n_dev; ++d)
-        NCCL_OK(ncclBroadcast((char*)reps[0].arena + off, (char*)reps[d].arena + off, cnt, ncclChar, 0, comms[d],
-                              st[d]));
-      NCCL_OK(ncclGroupEnd());
-    }
-    for (int d = 0; d < n_dev; ++d) {
-      HIP_OK(hipSetDevice(d));
-      HIP_OK(hipStreamSynchronize(st[d]));
-      HIP_OK(hipStreamDestroy(st[d]));
-      ncclCommDestroy(comms[d]);
+  const char* want = getenv("THALLAMA_REPLICATE");
+  RepPath path = n_rep == 1 ? RepPath::none : n_dev > 1 ? RepPath::rccl : RepPath::peer;
+  if (n_rep > 1 && want) {
+    if (!strcmp(want, "rccl")) path = RepPath::rccl;
+    else if (!strcmp(want, "peer")) path = RepPath::peer;
+    else if (!strcmp(want, "upload")) path = RepPath::upload;
+  }
+  const double t0 = now_s();
+  if (path == RepPath::rccl) {
+    // one communicator per GPU: replicas 0..n_dev-1 (all replicas when the choice was forced)
+    const int k = want && !strcmp(want, "rccl") ? n_rep : (n_dev < n_rep ? n_dev : n_rep);
+    const std::string err = rccl_broadcast(reps, k, m.bytes);
+    if (!err.empty()) {
+      printf("replication: RCCL failed (%s); falling back to peer copies\n", err.c_str());
+      path = RepPath::peer;
+    } else if (k < n_rep) {
+      const std::string e2 = peer_copies(reps, k, m.bytes);  // replicas sharing a GPU
+      if (!e2.empty()) {
+        printf("replication: %s; falling back to uploads\n", e2.c_str());
+        upload_each(m, reps, k);
+      }
     }
   }
-  for (int d = n_dev; d < n_rep; ++d) {
-    HIP_OK(hipSetDevice(reps[d].dev));
-    HIP_OK(hipMemcpy(reps[d].arena, reps[reps[d].dev].arena, m.bytes, hipMemcpyDeviceToDevice));
+  if (path == RepPath::peer) {
+    const std::string err = peer_copies(reps, 1, m.bytes);
+    if (!err.empty()) {
+      printf("replication: %s; falling back to uploads\n", err.c_str());
+      path = RepPath::upload;
+    }
   }
+  if (path == RepPath::upload) upload_each(m, reps, 1);
+  *used = path;
+  *rep_s = now_s() - t0;
+  assign_cpus(reps);
   for (int d = 0; d < n_rep; ++d) {
     Replica& r = reps[d];
     HIP_OK(hipSetDevice(r.dev));
@@ -292,10 +454,23 @@ static void release(std::vector<Replica>& reps) {
   }
 }
 
+// The scheduler's worker thread for replica r: pinned to r's core on its first callback.
+static int enter(Replica& r) {
+  thread_local int pinned = -1;
+  if (pinned != r.cpu && r.cpu >= 0) {
+    cpu_set_t one;
+    CPU_ZERO(&one);
+    CPU_SET(r.cpu, &one);
+    sched_setaffinity(0, sizeof one, &one);  // 0 = the calling thread
+    pinned = r.cpu;
+  }
+  return hipSetDevice(r.dev) == hipSuccess ? 0 : -3;
+}
+
 // test mode step callback: worker w drives replica w
 static int replica_step(void* ctx, int worker, int batch, const int* token, const int* pos, float* logits) {
   Replica& r = (*(std::vector<Replica>*)ctx)[worker];
-  if (hipSetDevice(r.dev) != hipSuccess) return -3;
+  if (enter(r)) return -3;
   (void)batch;
   const int st = thallama_decoder_forward(r.dec, token, pos, logits);
   if (st) fprintf(stderr, "device %d step: %s\n", r.dev, thallama_last_error());
@@ -305,7 +480,7 @@ static int replica_step(void* ctx, int worker, int batch, const int* token, cons
 // greedy test mode (-g 1): the argmax stays on the device and only the batch's ids come back
 static int replica_argmax(void* ctx, int worker, int batch, const int* token, const int* pos, int* next) {
   Replica& r = (*(std::vector<Replica>*)ctx)[worker];
-  if (hipSetDevice(r.dev) != hipSuccess) return -3;
+  if (enter(r)) return -3;
   (void)batch;
   const int st = thallama_decoder_step_argmax(r.dec, token, pos, next);
   if (st) fprintf(stderr, "device %d step: %s\n", r.dev, thallama_last_error());
@@ -317,7 +492,7 @@ static int replica_argmax(void* ctx, int worker, int batch, const int* token, co
 static int prefill_on(Replica& r, int slot, const int* tokens, int n, int pos0) {
   static const bool off = getenv("THALLAMA_NO_PREFILL") && atoi(getenv("THALLAMA_NO_PREFILL")) != 0;
   if (off) return 1;
-  if (hipSetDevice(r.dev) != hipSuccess) return -3;
+  if (enter(r)) return -3;
   const int st = thallama_decoder_prefill(r.dec, slot, tokens, n, pos0);
   if (st == (int)hipErrorNotSupported) return 1;
   if (st) fprintf(stderr, "device %d prefill: %s\n", r.dev, thallama_last_error());
@@ -428,7 +603,9 @@ int main(int argc, char* argv[]) {
   thallama_sampler* smp = thallama_sampler_create(V, temperature, topp, rng_seed);
 
   if (strcmp(mode, "generate") == 0) {
-    std::vector<Replica> reps = replicate(model, 1, 1, 1);
+    RepPath rp;
+    double rs;
+    std::vector<Replica> reps = replicate(model, 1, 1, 1, &rp, &rs);
     generate(model.cfg, reps[0], tok, smp, prompt, steps);
     release(reps);
   } else if (strcmp(mode, "chat") == 0) {
@@ -465,9 +642,16 @@ int main(int argc, char* argv[]) {
     fprintf(stderr, "\n Num Devices %d\n", n_rep);
     fprintf(stderr, "\n Batch Size %d\n", batch);
     const long load_start = time_in_ms();
-    std::vector<Replica> reps = replicate(model, n_dev, n_rep, batch);
-    fprintf(stdout, "\nLoad model time (1 %s + RCCL broadcast to %d GPUs): %f\n",
-            model.synth ? "on-device synthesis" : "upload", n_dev, (double)(time_in_ms() - load_start) / 1000);
+    RepPath rp;
+    double rep_s = 0.0;
+    std::vector<Replica> reps = replicate(model, n_dev, n_rep, batch, &rp, &rep_s);
+    const char* how = rp == RepPath::rccl ? "RCCL broadcast" : rp == RepPath::peer ? "peer copies"
+                      : rp == RepPath::upload ? "uploads" : "no copies";
+    fprintf(stdout, "replication: %s to %d replica(s) on %d GPU(s) in %f s\n", rep_name(rp), n_rep, n_dev, rep_s);
+    for (int w = 0; w < n_rep; ++w)
+      fprintf(stdout, "worker %d: device %d cpu %d\n", w, reps[w].dev, reps[w].cpu);
+    fprintf(stdout, "\nLoad model time (1 %s + %s to %d GPUs): %f\n", model.synth ? "on-device synthesis" : "upload",
+            how, n_dev, (double)(time_in_ms() - load_start) / 1000);
 
     for (int pass = 0; pass < passes; ++pass) {
       if (pass > 0) {  // a fresh copy of the requests (the scheduler fills in their outputs)
@@ -478,9 +662,13 @@ int main(int argc, char* argv[]) {
       }
       const long start = time_in_ms();
       long long num_gen_tokens = 0;
-      const int st = thallama_serve_requests_greedy(req, tokenizer_path, V, n_rep, batch, replica_step,
-                                                    getenv("THALLAMA_HOST_ARGMAX") ? nullptr : replica_argmax,
-                                                    replica_prefill, &reps, &num_gen_tokens);
+      std::vector<long long> w_tok((size_t)n_rep, 0);
+      std::vector<double> w_sec((size_t)n_rep, 0.0);
+      std::vector<int> w_req((size_t)n_rep, 0);
+      const int st = thallama_serve_requests_stats(req, tokenizer_path, V, n_rep, batch, replica_step,
+                                                   getenv("THALLAMA_HOST_ARGMAX") ? nullptr : replica_argmax,
+                                                   replica_prefill, &reps, &num_gen_tokens, w_tok.data(), w_sec.data(),
+                                                   w_req.data());
       const long end = time_in_ms();
       if (st != 0) {
         fprintf(stderr, "test mode failed (%d)\n", st);
@@ -488,6 +676,9 @@ int main(int argc, char* argv[]) {
       }
       if (passes > 1)
         fprintf(stdout, "pass %d: tokens %lld seconds %f\n", pass, num_gen_tokens, (double)(end - start) / 1000);
+      for (int w = 0; w < n_rep; ++w)  // per GPU (worker): its tokens, requests and busy time
+        fprintf(stdout, "pass %d worker %d device %d: tokens %lld requests %d seconds %f\n", pass, w, reps[w].dev,
+                w_tok[w], w_req[w], w_sec[w]);
       if (pass + 1 < passes) continue;
       fprintf(stdout, "Total achieved token: %lld\n", num_gen_tokens);
       fprintf(stdout, "elapsed time(s): %f, achieved throughput(tok/s): %f\n", (double)(end - start) / 1000,

@@ -18,7 +18,9 @@
 // inside a step, so a step can be captured into a hipGraph.
 #include <math.h>
 #include <string.h>
+#include <algorithm>
 #include <atomic>
+#include <deque>
 #include <functional>
 #include <map>
 #include <memory>
@@ -151,7 +153,6 @@ struct thallama_decoder {
   float2* rope_d = nullptr;
   float* xn_d = nullptr;        // [<=16][dim] normed rows for the matrix-core GEMV (batch >= 2)
   float* ssq_d = nullptr;       // [B][dim/16] per-tile sums of squares carried from Wo / W2 to the next norm
-  bool no_ssq = false;          // THALLAMA_NO_SSQ=1: the norm prologue launch instead (A/B measurement)
   bool ssq_carry = false;       // this step carries them (ssq_carry_ok)
   signed char* xq_d = nullptr;  // int8 batched: activations quantised once per launch [8][max(dim, hidden)]
   float* xqs_d = nullptr;       //   and their group scales
@@ -247,12 +248,7 @@ static void prof_collect(thallama_decoder* d) {
 
 static int auto_splits(const thallama_decoder* d) {
   // Enough (head, seq, split) blocks to cover the 256 CUs, at most 16 splits
-  // (THALLAMA_ATTN_SPLITS overrides, for measurements).
-  static const int forced = [] {
-    const char* e = getenv("THALLAMA_ATTN_SPLITS");
-    return e ? atoi(e) : 0;
-  }();
-  if (forced > 0) return forced > 16 ? 16 : forced;
+  // (THALLAMA_OPT_ATTN_SPLITS overrides per decoder, for measurements).
   // batches aim for 8 waves per CU: a unit walks its keys one 32-key chunk (one memory latency)
   // after another, so at B = 8 x 32 heads one unit per (b, h) left 256-step decodes latency-bound
   // (fp32 7B B=8: splits 1 / 2 / 4 / 8 / 16 -> 1366 / 1405 / 1414 / 1417 / 1417 tok/s)
@@ -271,28 +267,14 @@ static size_t granule_count(const thallama_decoder* d) {
   return (size_t)3 * d->dim + d->hidden + 2 * d->kv_dim + (size_t)d->H * d->S + 2;
 }
 
-// The batched persistent step (2..8 sequences, fp32): on unless THALLAMA_BATCH_PERSIST=0.
-// The batched persistent step (persist_b.hip) is prepared for 2..8 sequences unless
-// THALLAMA_BATCH_PERSIST=0, and taken BY DEFAULT for up to batch_persist_default_max() of them
-// (THALLAMA_OPT_PERSISTENT=1 selects it for the rest).  7B fp32 ms/step, persistent vs
-// multi-launch (profiles/r03/batch_persist_ab.json): B=2 4.69 vs 5.30, B=3 4.94 vs 7.04, B=4 5.21
-// vs 5.35, B=6 5.90 vs 5.59, B=8 6.57 vs 5.63 — past 4 sequences the all-gather hand-off of every
-// phase's input to every CU (B x K x 8 B of granules per CU per phase, 1.5 MB per layer at B=8)
-// costs more than the launches it saves; the matrix-core multi-launch kernels read K-split slices.
-static bool batch_persist_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("THALLAMA_BATCH_PERSIST");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-static int batch_persist_default_max() {
-  static const int v = [] {
-    const char* e = getenv("THALLAMA_BATCH_PERSIST");
-    return e && e[0] >= '1' && e[0] <= '9' ? atoi(e) : 4;
-  }();
-  return v;
-}
+// The batched persistent step (persist_b.hip) is prepared for 2..8 sequences and taken BY DEFAULT
+// for up to kBatchPersistDefaultMax of them (THALLAMA_OPT_PERSISTENT selects it, or the
+// multi-launch step, per decoder).  7B fp32 ms/step, persistent vs multi-launch
+// (profiles/r03/batch_persist_ab.json): B=2 4.69 vs 5.30, B=3 4.94 vs 7.04, B=4 5.21 vs 5.35, B=6
+// 5.90 vs 5.59, B=8 6.57 vs 5.63 — past 4 sequences the all-gather hand-off of every phase's input
+// to every CU (B x K x 8 B of granules per CU per phase, 1.5 MB per layer at B=8) costs more than
+// the launches it saves; the matrix-core multi-launch kernels read K-split slices.
+constexpr int kBatchPersistDefaultMax = 4;
 
 // Shapes the batched prefill handles (head size 64/128/256, rows in multiples of 32).
 static bool prefill_shape_ok(const thallama_decoder* d) {
@@ -358,8 +340,6 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
     TL_TRY(hipMalloc(&d->xn_d, sizeof(float) * (size_t)(batch < 16 ? batch : 16) * d->dim));
     TL_TRY(hipMalloc(&d->ssq_d, sizeof(float) * (size_t)batch * ((d->dim + 15) / 16)));
     TL_TRY(hipMemset(d->ssq_d, 0, sizeof(float) * (size_t)batch * ((d->dim + 15) / 16)));
-    const char* e = getenv("THALLAMA_NO_SSQ");
-    d->no_ssq = e && e[0] == '1';
     TL_TRY(hipMalloc(&d->mpart_d, sizeof(float) * nblk * 2 * 256));
     TL_TRY(hipMalloc(&d->mcnt_d, sizeof(unsigned) * nblk));
     TL_TRY(hipMemset(d->mcnt_d, 0, sizeof(unsigned) * nblk));
@@ -384,9 +364,9 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
     const char* why = nullptr;
     if (batch == 1) {
       d->pok = tl::persistent_prepare(ps, d->ncu, &why);
-    } else if (batch <= 8 && batch_persist_enabled()) {
+    } else if (batch <= 8) {
       d->pok = tl::persistent_prepare_b(ps, d->ncu, &why);
-      d->persist = batch <= batch_persist_default_max();
+      d->persist = batch <= kBatchPersistDefaultMax;
     } else {
       why = batch > 8 ? "batch > 8" : "THALLAMA_BATCH_PERSIST=0";
     }
@@ -532,7 +512,7 @@ static int q8_attn_quant(const thallama_decoder* d) {
 // would then read sums the previous step or another layer left.  Consumers that do not take the
 // matrix path ignore ssq_in (the streaming kernels normalise from x).
 static bool ssq_carry_ok(const thallama_decoder* d) {
-  if (d->q8 || !d->ssq_d || d->no_ssq || (d->dim + 15) / 16 > 256) return false;  // (the kernel sums <= 256 tiles)
+  if (d->q8 || !d->ssq_d || (d->dim + 15) / 16 > 256) return false;  // (the kernel sums <= 256 tiles)
   for (int l = 0; l < d->L; ++l) {
     tl::GemvParams wo = {}, w2 = {};
     wo.W0 = d->w.wo + (long long)l * d->dim * d->dim;
@@ -1191,8 +1171,11 @@ extern "C" double thallama_step_bytes(const Config* c, int B, int kclass, const 
 // ------------------------------------------------------------------ thaDNN_s_forward_batch
 // The reference signature carries no workspace, so a decoder per (device, stream, batch, config,
 // fp32|int8) is created on first use and reused.  A call with other weight / state buffers than
-// the cached decoder's replaces it, and at most kDecCacheMax decoders stay cached (least recently
-// used evicted), so a host that reallocates its buffers does not grow without bound.
+// the cached decoder's replaces it, and at most g_dec_cap decoders stay cached (least recently
+// used evicted), so a host that reallocates its buffers does not grow without bound.  The cap
+// starts at 8 and follows the caller's working set: a miss on a key evicted recently (a "ghost")
+// means the cache was too small for the keys in use — e.g. the reference's pipeline test, 4 host
+// threads x n_devices stage decoders (src/llama.cpp:1298) — and raises the cap by one, up to 256.
 // The reference calls this entry from one host thread per GPU (src/llama.cpp:919, 1017), so
 // entries are shared: a caller holds a reference (shared_ptr) for the whole forward, eviction only
 // drops the cache's reference, and the decoder is destroyed when its last user returns; callers
@@ -1213,13 +1196,17 @@ struct DecEntry {
   std::shared_ptr<CachedDecoder> c;
   unsigned long long used;
 };
-constexpr size_t kDecCacheMax = 8;
+constexpr size_t kDecCacheMin = 8, kDecCacheCeil = 256;
+size_t g_dec_cap = kDecCacheMin;
+std::deque<DecKey> g_dec_ghosts;  // recently evicted keys, oldest first (at most kDecCacheCeil)
 std::mutex g_dec_mu;
 unsigned long long g_dec_clock = 0;
 std::atomic<long long> g_dec_live{0};  // decoders alive (cached or still in use after eviction)
+// Allocated once and never freed: decoders still cached at process exit are not destroyed during
+// static destruction (after HIP's own teardown, with the lock object possibly gone).
 std::map<DecKey, DecEntry>& dec_cache() {
-  static std::map<DecKey, DecEntry> m;
-  return m;
+  static auto* m = new std::map<DecKey, DecEntry>();
+  return *m;
 }
 
 // The cached decoder for key, if it was made for exactly these buffers; else a new one (replacing
@@ -1237,11 +1224,19 @@ std::shared_ptr<CachedDecoder> dec_lookup(const DecKey& key, const Config* p, co
       return it->second.c;
     }
     m.erase(it);  // destroyed now, or when its last user returns
+  } else {
+    auto gh = std::find(g_dec_ghosts.begin(), g_dec_ghosts.end(), key);
+    if (gh != g_dec_ghosts.end()) {  // thrashing: the working set is larger than the cap
+      g_dec_ghosts.erase(gh);
+      if (g_dec_cap < kDecCacheCeil) ++g_dec_cap;
+    }
   }
-  while (m.size() >= kDecCacheMax) {
+  while (m.size() >= g_dec_cap) {
     auto lru = m.begin();
     for (auto i = m.begin(); i != m.end(); ++i)
       if (i->second.used < lru->second.used) lru = i;
+    g_dec_ghosts.push_back(lru->first);
+    if (g_dec_ghosts.size() > kDecCacheCeil) g_dec_ghosts.pop_front();
     m.erase(lru);
   }
   thallama_decoder* d = nullptr;
@@ -1263,6 +1258,11 @@ std::shared_ptr<CachedDecoder> dec_lookup(const DecKey& key, const Config* p, co
 extern "C" int thallama_forward_batch_cache_size(void) {
   std::lock_guard<std::mutex> g(g_dec_mu);
   return (int)dec_cache().size();
+}
+
+extern "C" int thallama_forward_batch_cache_cap(void) {
+  std::lock_guard<std::mutex> g(g_dec_mu);
+  return (int)g_dec_cap;
 }
 
 // Decoders alive: the cached ones plus evicted ones a caller is still running.
@@ -1745,6 +1745,11 @@ extern "C" int thallama_decoder_prefill(thallama_decoder* d, int b, const int* t
       g_last_error = "thallama_decoder_prefill: token out of range";
       return (int)hipErrorInvalidValue;
     }
+  // the pinned staging may still feed a copy in flight (an earlier call that returned early, or an
+  // asynchronous greedy call), and a persistent give-up of an asynchronous call is reported before
+  // this call writes any K/V row (as upload_tok_pos does for the decode steps)
+  TL_TRY(hipStreamSynchronize(d->stream));
+  if (const int r = check_async(d)) return r;
   if (d->q8) return prefill_q8(d, b, tokens_h, n, pos0);
   const int CH = kPrefillChunk, dim = d->dim, hid = d->hidden, kvd = d->kv_dim, S = d->S;
   const int max_ns = kPrefillMaxSplits;
@@ -1757,7 +1762,7 @@ extern "C" int thallama_decoder_prefill(thallama_decoder* d, int b, const int* t
   float* kc_b = d->s.key_cache + (long long)b * kv_b_stride;
   float* vc_b = d->s.value_cache + (long long)b * kv_b_stride;
   hipStream_t st = d->stream;
-  // the prompt's ids through pinned staging (the previous call ended with a synchronisation)
+  // the prompt's ids through pinned staging (idle: synchronised above)
   memcpy(d->pf_tok_h, tokens_h, sizeof(int) * n);
   TL_TRY(hipMemcpyAsync(d->pf_tok, d->pf_tok_h, sizeof(int) * n, hipMemcpyHostToDevice, st));
   for (int c = 0, m = 0; c < n; c += m) {

@@ -88,14 +88,13 @@ struct GemvParams {
   int ssq_nt;            // tiles of the producing launch (its rows / 16)
 };
 
-// Blocks the matrix-core GEMV aims for: kMfmaDepth per CU (env THALLAMA_MFMA_DEPTH).
+// Blocks the matrix-core GEMV aims for: 4 per CU (6 and 8 lost 12-15% everywhere, 2 wins only for
+// the residual launch with K <= 4096, mfma_splits' depth2).
 inline int mfma_target_blocks() {
   static const int v = [] {
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    const char* e = getenv("THALLAMA_MFMA_DEPTH");
-    const int depth = e ? atoi(e) : 4;
-    return ncu * (depth > 0 ? depth : 1);
+    return ncu * 4;
   }();
   return v;
 }

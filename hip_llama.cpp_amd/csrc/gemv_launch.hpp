@@ -8,15 +8,8 @@
 
 namespace tl {
 
-// Smallest batch that takes the matrix-core GEMV (env THALLAMA_MFMA_MIN_NB overrides; a
-// value above 16 disables it).
-inline int gemv_mfma_min_nb() {
-  static const int v = [] {
-    const char* e = getenv("THALLAMA_MFMA_MIN_NB");
-    return e ? atoi(e) : 4;
-  }();
-  return v;
-}
+// Smallest batch that takes the matrix-core GEMV.
+constexpr int kMfmaMinNb = 4;
 
 // Split K across blocks when the row tiles alone leave CUs idle: msplit = target / tiles,
 // at least 2 steps per wave per split; needs the decoder's mpart/mcnt scratch, sized for
@@ -26,7 +19,7 @@ inline int gemv_mfma_min_nb() {
 // everywhere: tools/job_r02_depth.sh).
 inline void mfma_splits(GemvParams& p, int tiles, bool depth2 = false) {
   const int nsteps = p.K >> 4;
-  int ms = p.mpart && p.mcnt ? mfma_target_blocks() / (depth2 && !getenv("THALLAMA_MFMA_DEPTH") ? 2 : 1) / tiles : 1;
+  int ms = p.mpart && p.mcnt ? mfma_target_blocks() / (depth2 ? 2 : 1) / tiles : 1;
   const int cap = nsteps / (2 * kMfmaWaves);
   if (ms > cap) ms = cap;
   if (ms < 1) ms = 1;
@@ -35,17 +28,11 @@ inline void mfma_splits(GemvParams& p, int tiles, bool depth2 = false) {
 }
 
 // The register-resident batched GEMV (gemv_rr.hpp) when the rows fill every CU and a block's rows
-// fit its LDS partials, for up to rr_max_nb() sequences: 4 by default (7B fp32 B=4: 740 vs 726
-// tok/s on the matrix-core kernel; at 8 sequences it measured slower, 1255-1328 vs 1408-1433,
-// tools/job_r02_t.sh), env THALLAMA_GEMV_RR=N moves the bound (0 = never).  Same ssq contract
-// as the matrix-core kernel, so the two mix freely within a step.
-inline int rr_max_nb() {
-  static const int v = [] {
-    const char* e = getenv("THALLAMA_GEMV_RR");
-    return e ? atoi(e) : 4;
-  }();
-  return v;
-}
+// fit its LDS partials, for up to kRrMaxNb sequences (7B fp32 B=4: 740 vs 726 tok/s on the
+// matrix-core kernel; at 8 sequences it measured slower, 1255-1328 vs 1408-1433,
+// profiles/jobs/job_r02_t.sh).  Same ssq contract as the matrix-core kernel, so the two mix freely
+// within a step.
+constexpr int kRrMaxNb = 4;
 
 inline int rr_grid() {
   static const int v = [] {
@@ -59,7 +46,7 @@ inline int rr_grid() {
 template <int MODE>
 inline bool rr_ok(const GemvParams& p) {
   const int G = rr_grid();
-  if (p.nb > rr_max_nb() || p.nb > 8 || (p.K & 255) || (p.x_stride & 3)) return false;
+  if (p.nb > kRrMaxNb || p.nb > 8 || (p.K & 255) || (p.x_stride & 3)) return false;
   constexpr int RPI = RowsPerItem<MODE>::v;
   const long long rows = (long long)p.n_items * RPI;
   if (rows < 16LL * G) return false;
@@ -114,11 +101,11 @@ inline hipError_t launch_nb(const GemvParams& p, hipStream_t s, const GemvCfg& c
 
 // The shape half of the matrix-core / register-resident selection (the norm half is the
 // prologue test in launch_mode): whole 1-KiB wave-loads, 16-float k steps, aligned rows, and
-// at least gemv_mfma_min_nb() sequences in every 16-sequence group launch_mode cuts.
+// at least kMfmaMinNb sequences in every 16-sequence group launch_mode cuts.
 inline bool matrix_path_ok(const GemvParams& p) {
   if (p.n_items <= 0 || p.nb <= 0 || !gemv_fast_ok(p) || (p.K & 15) || (p.x_stride & 3)) return false;
   for (int b0 = 0; b0 < p.nb; b0 += 16)
-    if ((p.nb - b0 < 16 ? p.nb - b0 : 16) < gemv_mfma_min_nb()) return false;
+    if ((p.nb - b0 < 16 ? p.nb - b0 : 16) < kMfmaMinNb) return false;
   return true;
 }
 

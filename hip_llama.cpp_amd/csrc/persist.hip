@@ -40,12 +40,10 @@
 
 namespace tl {
 
-#ifndef PERSIST_NBUF
-#define PERSIST_NBUF 2
-#endif
-// Register slots in flight per streaming wave.  2: 9 waves (3 on one SIMD, <= 168 VGPRs);
-// 4: 8 waves (2 per SIMD, <= 256 VGPRs), i.e. 28 instead of 16 slots in flight per CU.
-constexpr int NBUF = PERSIST_NBUF;
+// Register slots in flight per streaming wave: 2, with 9 waves (3 on one SIMD, <= 168 VGPRs).  4
+// register slots with 8 waves (28 instead of 16 slots in flight per CU) spilled and lost 1-8%
+// (DESIGN.md §3); the knob that built it is gone.
+constexpr int NBUF = 2;
 // Buffers refilled with the next phase's slots before its staging (the rest right after it).
 // A wave's loads return in order, so its granule sweep waits behind what it prefetched: with
 // int8 weights (short phases, the hand-off dominates) one buffer is best (+2.2% over two),
@@ -59,12 +57,7 @@ constexpr int NSW = PW - 1;  // streaming waves per block
 constexpr int SB = 2;        // staged float4 per thread and batch (granule loads in flight; profiles/r04/persist_knobs_ab.txt)
 constexpr int kPResidFloats = 256;  // residual-stream slice per block (LDS)
 constexpr unsigned kSpinLimit = 1u << 18;
-#ifndef PERSIST_ATTN_CH
-#define PERSIST_ATTN_CH 16  // keys per attention chunk (one memory latency each) in the control wave
-#endif
-#ifndef PERSIST_ATTN_WIN
-#define PERSIST_ATTN_WIN 1  // fp32: attention units with their keys in LDS windows (attn_unit_win)
-#endif
+// fp32 attention units keep their keys in LDS windows (attn_unit_win).
 // From kAttnHelpMinKeys keys on (fp32, batch 1; persist.hpp), the attention phase runs twice as
 // many units (key splits) per head: one on each block's control wave and one on streaming wave 1,
 // whose window is the staging strip (free between the QKV and Wo stagings).  One wave keeps at
@@ -72,10 +65,7 @@ constexpr unsigned kSpinLimit = 1u << 18;
 // The helper lives in its own kernel instantiation (HELP), launched only at such positions: its
 // registers (the streaming wave's slots stay live across the unit) spill 20 B in the shared
 // code, which cost the short-context step 1.2% (profiles/r04/attn_help_ab.txt).
-#ifndef PERSIST_XCD_SKEW
-#define PERSIST_XCD_SKEW 4
-#endif
-constexpr unsigned kXcdSkew = PERSIST_XCD_SKEW;  // percent (geo)
+constexpr unsigned kXcdSkew = 4;  // percent (geo); 2 / 6 / 8 measured no better (profiles/r04/xcd_skew_sweep.txt)
 #define TL_HOST_DEVICE_INLINE __host__ __device__ inline
 
 enum PKind : int { PK_QKV = 0, PK_ATTN = 1, PK_WO = 2, PK_UP = 3, PK_DOWN = 4, PK_CLS = 5 };
@@ -842,10 +832,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
         } else {
           // long contexts: twice the splits, the second unit of each block on streaming wave 1
           const int units = p.H * aw.NS;
-          for (int u = blockIdx.x; u < units; u += (help ? 2 : 1) * G) {
-            if constexpr (PERSIST_ATTN_WIN) attn_unit_win<HS>(aw, u, awin, lane);
-            else attn_unit<HS, PERSIST_ATTN_CH, true>(aw, u, lane);
-          }
+          for (int u = blockIdx.x; u < units; u += (help ? 2 : 1) * G) attn_unit_win<HS>(aw, u, awin, lane);
           if (help) __syncthreads();  // the helper's window (the strip) is free for the Wo staging
         }
         TRACE(3);
@@ -884,7 +871,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
       const int l = ph / 5;
       const int kind = ph == nph - 1 ? PK_CLS : ph % 5;
       if (kind == PK_ATTN) {
-        if constexpr (!Q8 && PERSIST_ATTN_WIN) {
+        if constexpr (!Q8) {
           if (HELP && p.attn_help && p.pos[0] + 1 >= kAttnHelpMinKeys) {
             if (sw == 0) {  // the block's second attention unit (control wave: the first)
               AttnWaveParams aw = {};
@@ -1002,7 +989,7 @@ constexpr size_t kDynLdsCap = 160 * 1024;  // dynamic LDS per block (gfx950: 160
 static size_t lds_bytes(const PStep& p) {
   return (size_t)(kPResidFloats + kPResFloats + 16 + p.dim + p.pad_floats) * 4 + (size_t)p.q8_pad +
          (size_t)p.q8_pad / 16 + (size_t)(p.n_sqa + p.n_scr + p.n_cw) * 4 + 32 * 8 +
-         (p.q8 || !PERSIST_ATTN_WIN ? 0 : (size_t)attn_win_floats(p.hs) * 4);
+         (p.q8 ? 0 : (size_t)attn_win_floats(p.hs) * 4);
 }
 
 template <int HS, bool Q8, bool HELP = false>
@@ -1084,7 +1071,7 @@ bool persistent_prepare(PStep& p, int ncu, const char** why) {
   }
   if (lds_bytes(p) > kDynLdsCap) return fail("activations do not fit the LDS");
   p.attn_help = 0;
-  if (!p.q8 && PERSIST_ATTN_WIN && p.NS * 2 <= kMaxNS) {  // room for a second attention window in the strip?
+  if (!p.q8 && p.NS * 2 <= kMaxNS) {  // room for a second attention window in the strip?
     const int base = p.pad_floats, need = attn_win_floats(p.hs);
     if (base < need) p.pad_floats = need;
     if (lds_bytes(p) <= kDynLdsCap) p.attn_help = 1;

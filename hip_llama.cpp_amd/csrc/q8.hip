@@ -17,14 +17,6 @@ namespace tl {
 
 static inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-// The int8 matrix-core GEMV for 4..8 sequences (env THALLAMA_Q8_MFMA=0 turns it off).
-static bool q8_mfma_enabled() {
-  static const bool v = [] {
-    const char* e = getenv("THALLAMA_Q8_MFMA");
-    return !e || atoi(e) != 0;
-  }();
-  return v;
-}
 
 bool gemv_q8_fast_ok(const GemvParams& p) {
   if (p.K <= 0 || p.gs < 32 || p.gs > 128 || (p.gs & (p.gs - 1)) || p.K % p.gs || (p.K & 15)) return false;
@@ -153,7 +145,7 @@ static hipError_t launch_q8_mode(const GemvParams& p0, hipStream_t s, bool nt) {
     } else {
       p.xq = nullptr;
     }
-    if (p.nb >= 4 && p.xq && p.gs == 64 && (p.K & 255) == 0 && q8_mfma_enabled()) {
+    if (p.nb >= 4 && p.xq && p.gs == 64 && (p.K & 255) == 0) {
       // 4..8 sequences: the int8 matrix-core kernel (gemv_q8_mfma.hpp), K split across blocks
       // like the fp32 one (in 256-byte runs)
       const int rows = MODE == GM_QKV ? 2 * p.n_items : p.n_items;

@@ -163,16 +163,37 @@ extern "C" void free_transformer(Transformer* t) {
 }
 
 // ------------------------------------------------------------------ device residency
+// A host-to-device copy outside the process lock: ordered on a private non-blocking stream, so it
+// neither disturbs another thread's capture nor blocks the other threads for its duration (a 7B
+// model is 27 GB; the reference uploads from one host thread per GPU at once, src/llama.cpp:919-943).
+// Only the stream's creation and destruction take the lock.
+static void h2d_private(void* dst, const void* src, size_t bytes) {
+  hipStream_t st = nullptr;
+  {
+    tl::ApiLock lock(tl::api_mu());
+    CHECK_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  }
+  CHECK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st));
+  CHECK_HIP(hipStreamSynchronize(st));
+  tl::ApiLock lock(tl::api_mu());
+  CHECK_HIP(hipStreamDestroy(st));
+}
+
+static void* dev_alloc(size_t bytes) {
+  void* a = nullptr;
+  tl::ApiLock lock(tl::api_mu());
+  CHECK_HIP(hipMalloc(&a, bytes));
+  return a;
+}
+
 // reference src/models.cpp:86-127: one arena, one copy (the payload is contiguous after the
 // header in a v0 file, src/utils.cpp:119-177)
 extern "C" void copy_weight_to_device(Transformer* t_h, TransformerWeights*& w_d) {
   const Config* p = &t_h->config;
   const int shared = t_h->weights.wcls == t_h->weights.token_embedding_table;
   const size_t n = thallama_v0_payload_floats(p, shared);
-  float* arena = nullptr;
-  tl::ApiLock lock(tl::api_mu());
-  CHECK_HIP(hipMalloc(&arena, n * sizeof(float)));
-  CHECK_HIP(hipMemcpy(arena, t_h->weights.token_embedding_table, n * sizeof(float), hipMemcpyHostToDevice));
+  float* arena = (float*)dev_alloc(n * sizeof(float));
+  h2d_private(arena, t_h->weights.token_embedding_table, n * sizeof(float));
   w_d = (TransformerWeights*)malloc(sizeof(TransformerWeights));
   thallama_map_weights(w_d, p, arena, shared);
 }
@@ -259,14 +280,12 @@ static TransformerWeights* upload_pipeline_weights(const Transformer* t_h, int p
       {h.w3 + l0 * dim * hid, P * dim * hid}, {h.rms_final_weight, dim}, {h.wcls, shared ? 0 : V * dim}};
   size_t total = 0;
   for (const auto& e : part) total += e.n;
-  float* arena = nullptr;
-  tl::ApiLock lock(tl::api_mu());
-  CHECK_HIP(hipMalloc(&arena, total * sizeof(float)));
+  float* arena = (float*)dev_alloc(total * sizeof(float));
   float* dst[12];
   size_t off = 0;
   for (int i = 0; i < 12; ++i) {
     dst[i] = arena + off;
-    if (part[i].n) CHECK_HIP(hipMemcpy(dst[i], part[i].src, part[i].n * sizeof(float), hipMemcpyHostToDevice));
+    if (part[i].n) h2d_private(dst[i], part[i].src, part[i].n * sizeof(float));
     off += part[i].n;
   }
   TransformerWeights* w = (TransformerWeights*)calloc(1, sizeof(TransformerWeights));
@@ -401,21 +420,19 @@ extern "C" void alloc_weight_to_device_70B(Transformer* h_t, TransformerWeights*
   const size_t layer = 2 * dim + 2 * dim * dim + 2 * dim * kvd + 3 * dim * hid;
   const TransformerWeights& h = h_t->weights;
   const bool shared = h.wcls == h.token_embedding_table;
-  float* a = nullptr;
-  tl::ApiLock lock(tl::api_mu());
-  CHECK_HIP(hipMalloc(&a, (V * dim + dim + (shared ? 0 : V * dim) + 2 * layer) * sizeof(float)));
+  float* a = (float*)dev_alloc((V * dim + dim + (shared ? 0 : V * dim) + 2 * layer) * sizeof(float));
   d_w = (TransformerWeights*)calloc(1, sizeof(TransformerWeights));
   d_w->token_embedding_table = a;
-  CHECK_HIP(hipMemcpy(a, h.token_embedding_table, V * dim * sizeof(float), hipMemcpyHostToDevice));
+  h2d_private(a, h.token_embedding_table, V * dim * sizeof(float));
   a += V * dim;
   d_w->rms_final_weight = a;
-  CHECK_HIP(hipMemcpy(a, h.rms_final_weight, dim * sizeof(float), hipMemcpyHostToDevice));
+  h2d_private(a, h.rms_final_weight, dim * sizeof(float));
   a += dim;
   if (shared) {
     d_w->wcls = d_w->token_embedding_table;
   } else {
     d_w->wcls = a;
-    CHECK_HIP(hipMemcpy(a, h.wcls, V * dim * sizeof(float), hipMemcpyHostToDevice));
+    h2d_private(a, h.wcls, V * dim * sizeof(float));
     a += V * dim;
   }
   float** f[9] = {&d_w->rms_att_weight, &d_w->rms_ffn_weight, &d_w->wq, &d_w->wk, &d_w->wv, &d_w->wo, &d_w->w1,

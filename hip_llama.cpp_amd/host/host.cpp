@@ -20,6 +20,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <chrono>
 #include <fstream>
 #include <mutex>
 #include <string>
@@ -316,6 +317,15 @@ extern "C" int thallama_serve_requests_greedy(thallama_requests* r, const char* 
                                               int n_workers, int batch, thallama_step_fn step,
                                               thallama_argmax_step_fn argmax_step, thallama_prefill_fn prefill,
                                               void* ctx, long long* gen_tokens) {
+  return thallama_serve_requests_stats(r, tokenizer_path, vocab_size, n_workers, batch, step, argmax_step, prefill, ctx,
+                                       gen_tokens, nullptr, nullptr, nullptr);
+}
+
+extern "C" int thallama_serve_requests_stats(thallama_requests* r, const char* tokenizer_path, int vocab_size,
+                                             int n_workers, int batch, thallama_step_fn step,
+                                             thallama_argmax_step_fn argmax_step, thallama_prefill_fn prefill,
+                                             void* ctx, long long* gen_tokens, long long* worker_tokens,
+                                             double* worker_seconds, int* worker_requests) {
   if (!r || n_workers <= 0 || batch <= 0) return -1;
   // greedy sampling is sample_argmax of the logits: the device step may take it (only B ids return)
   const bool on_device = argmax_step && r->temperature == 0.0f;
@@ -329,7 +339,9 @@ extern "C" int thallama_serve_requests_greedy(thallama_requests* r, const char* 
   std::atomic<long long> gen{0};
   std::atomic<int> status{0};
 
+  const auto t_start = std::chrono::steady_clock::now();
   auto worker = [&](int w) {
+    int served = 0;
     thallama_tokenizer* tok = thallama_tokenizer_load(tokenizer_path, V);
     if (!tok) {
       status = -2;
@@ -419,6 +431,7 @@ extern "C" int thallama_serve_requests_greedy(thallama_requests* r, const char* 
         r->outputs[req[b]] = text[b].substr(0, r->cap() > 0 ? r->cap() - 1 : 0);
         fprintf(stderr, "\nThread %d DONE Request %d \n", w, req[b]);
         local += pos[b] - 1;
+        ++served;
         req[b] = -1;
         done[b] = 0;
         pos[b] = 0;
@@ -426,6 +439,12 @@ extern "C" int thallama_serve_requests_greedy(thallama_requests* r, const char* 
       }
     }
     gen += local;
+    // per-worker accounting (one worker = one GPU's replica): its tokens, its requests, and the
+    // time from the common start to its last step
+    if (worker_tokens) worker_tokens[w] = local;
+    if (worker_requests) worker_requests[w] = served;
+    if (worker_seconds)
+      worker_seconds[w] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
     thallama_tokenizer_free(tok);
   };
 

@@ -194,6 +194,7 @@ def lib():
             "alloc_weight_to_device_70B": (None, [C.POINTER(Transformer), C.POINTER(C.POINTER(TransformerWeights))]),
             "free_weight_device": (None, [C.POINTER(TransformerWeights)]),
             "thallama_forward_batch_cache_size": (I, []),
+            "thallama_forward_batch_cache_cap": (I, []),
             "thallama_forward_batch_live": (I, []),
             "thallama_forward_batch_cache_clear": (None, []),
             "thallama_synth_arena": (I, [P, C.POINTER(Config), I, C.c_uint64, VP]),

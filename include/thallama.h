@@ -134,13 +134,16 @@ void thallama_decoder_prof_reset(thallama_decoder* d);
 int thallama_decoder_stage(thallama_decoder* d, const int* token_h, const int* pos_h, int embed, float* logits_h,
                            const thallama_decoder* wait, float* x_next, int next_dev);
 
-/* thaDNN_s_forward_batch / thaDNN_q8_forward_batch keep one decoder per (device, stream, batch,
- * config, dtype), made for the caller's weight and state buffers; a call with other buffers
- * replaces it, and at most 8 stay cached (least recently used dropped).  Concurrent callers are
- * safe: a dropped decoder is freed when the last call using it returns.  The cached count, the
- * live count (cached + dropped but still running), and a way to drop them all (e.g. before the
- * caller frees its buffers). */
+/* thaDNN_s_forward_batch / thaDNN_q8_forward_batch (and the pipeline drivers' stage decoders) keep
+ * one decoder per (device, stream, batch, config, dtype), made for the caller's weight and state
+ * buffers; a call with other buffers replaces it, and at most cap stay cached (least recently used
+ * dropped; the cap starts at 8 and grows by one, up to 256, whenever a recently dropped key comes
+ * back, so it follows the callers' working set).  Concurrent callers are safe: a dropped decoder is
+ * freed when the last call using it returns.  The cached count, the cap, the live count (cached +
+ * dropped but still running), and a way to drop them all (e.g. before the caller frees its
+ * buffers). */
 int thallama_forward_batch_cache_size(void);
+int thallama_forward_batch_cache_cap(void);
 int thallama_forward_batch_live(void);
 void thallama_forward_batch_cache_clear(void);
 

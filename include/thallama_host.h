@@ -92,6 +92,14 @@ typedef int (*thallama_argmax_step_fn)(void* ctx, int worker, int batch, const i
 int thallama_serve_requests_greedy(thallama_requests* r, const char* tokenizer_path, int vocab_size, int n_workers,
                                    int batch, thallama_step_fn step, thallama_argmax_step_fn argmax_step,
                                    thallama_prefill_fn prefill, void* ctx, long long* gen_tokens);
+/* thallama_serve_requests_greedy with per-worker accounting (each array n_workers long, any may be
+ * NULL): worker w's share of *gen_tokens, the requests it finished, and the seconds from the
+ * common start to its last step — one worker per GPU, so these are the per-GPU numbers of a
+ * multi-GPU run. */
+int thallama_serve_requests_stats(thallama_requests* r, const char* tokenizer_path, int vocab_size, int n_workers,
+                                  int batch, thallama_step_fn step, thallama_argmax_step_fn argmax_step,
+                                  thallama_prefill_fn prefill, void* ctx, long long* gen_tokens,
+                                  long long* worker_tokens, double* worker_seconds, int* worker_requests);
 
 #ifdef __cplusplus
 }

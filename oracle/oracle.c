@@ -53,6 +53,7 @@ typedef struct {
   OQT xq, hq;
   float *k, *v;
   int view; /* 1: a second decoder over another model's weights (owns its RunState only) */
+  double *kc64, *vc64; /* forward_f64's own K/V rows (flag kF64OwnCache), lazily allocated */
 } OModel;
 
 static int g_threads = 1;
@@ -257,6 +258,8 @@ int oracle_write_v0(OModel* m, const char* path) {
 
 void oracle_model_free(OModel* m) {
   if (!m) return;
+  free(m->kc64);
+  free(m->vc64);
   if (m->view) {
     free(m->x); free(m->xb); free(m->xb2); free(m->hb); free(m->hb2); free(m->q);
     free(m->att); free(m->logits); free(m->kc); free(m->vc); free(m->k); free(m->v);
@@ -334,7 +337,29 @@ static void rmsnorm_f64(double* o, const double* x, const float* weight, int siz
   for (int j = 0; j < size; j++) o[j] = (double)weight[j] * (ss * x[j]);
 }
 
-int oracle_forward_f64(OModel* m, int token, int pos, double* logits) {
+/* flags: kF64RopeDouble — RoPE's (cos, sin) computed in double like every other quantity (default:
+ * the reference's float values, which its fp32 forward and the GPU use); kF64OwnCache — the K/V rows
+ * of earlier positions from this function's own double cache (written at every call) instead of the
+ * fp32 cache.  With both, this is the reference's src/seq.cpp widened to double, which
+ * oracle/ref_f64_driver.cpp builds from the reference source itself
+ * (tests/test_oracle.py::test_forward_f64_matches_widened_reference). */
+enum { kF64RopeDouble = 1, kF64OwnCache = 2 };
+static int forward_f64_impl(OModel* m, int token, int pos, double* logits, int flags);
+int oracle_forward_f64(OModel* m, int token, int pos, double* logits) { return forward_f64_impl(m, token, pos, logits, 0); }
+int oracle_forward_f64_ex(OModel* m, int token, int pos, double* logits, int flags) {
+  return forward_f64_impl(m, token, pos, logits, flags);
+}
+
+static int forward_f64_impl(OModel* m, int token, int pos, double* logits, int flags) {
+  const int rope_double = flags & kF64RopeDouble;
+  const size_t cache_n = (size_t)m->c.n_layers * m->c.seq_len * ((size_t)m->c.dim * m->c.n_kv_heads / m->c.n_heads);
+  if ((flags & kF64OwnCache) && !m->kc64) {
+    m->kc64 = (double*)calloc(cache_n, sizeof(double));
+    m->vc64 = (double*)calloc(cache_n, sizeof(double));
+    if (!m->kc64 || !m->vc64) return -1;
+  }
+  const double* kc64 = (flags & kF64OwnCache) ? m->kc64 : NULL;
+  const double* vc64 = (flags & kF64OwnCache) ? m->vc64 : NULL;
   const OCfg* p = &m->c;
   const int dim = p->dim, hid = p->hidden_dim, hs = dim / p->n_heads;
   const int kvd = (p->dim * p->n_kv_heads) / p->n_heads, kv_mul = p->n_heads / p->n_kv_heads;
@@ -358,9 +383,17 @@ int oracle_forward_f64(OModel* m, int token, int pos, double* logits) {
     matmul_f64(v, xb, m->wv + L * dim * kvd, dim, kvd);
     for (int i = 0; i < dim; i += 2) {
       const int head_dim = i % hs;
-      const float freq = 1.0f / powf(10000.0f, head_dim / (float)hs);
-      const float val = pos * freq;
-      const double fcr = cosf(val), fci = sinf(val);
+      double fcr, fci;
+      if (rope_double) {
+        const double freq = 1.0 / pow(10000.0, head_dim / (double)hs), val = pos * freq;
+        fcr = cos(val);
+        fci = sin(val);
+      } else {
+        const float freq = 1.0f / powf(10000.0f, head_dim / (float)hs);
+        const float val = pos * freq;
+        fcr = cosf(val);
+        fci = sinf(val);
+      }
       for (int r = 0; r < (i < kvd ? 2 : 1); r++) {
         double* vec = r == 0 ? q : k;
         const double v0 = vec[i], v1 = vec[i + 1];
@@ -369,6 +402,10 @@ int oracle_forward_f64(OModel* m, int token, int pos, double* logits) {
       }
     }
     const size_t loff = L * p->seq_len * (size_t)kvd;
+    if (flags & kF64OwnCache) {
+      memcpy(m->kc64 + loff + (size_t)pos * kvd, k, sizeof(double) * kvd);
+      memcpy(m->vc64 + loff + (size_t)pos * kvd, v, sizeof(double) * kvd);
+    }
     for (int h = 0; h < p->n_heads; h++) {
       const double* qh = q + h * hs;
       const int off = (h / kv_mul) * hs;
@@ -376,7 +413,9 @@ int oracle_forward_f64(OModel* m, int token, int pos, double* logits) {
       for (int t = 0; t <= pos; t++) {
         double sc = 0.0;
         for (int i = 0; i < hs; i++)
-          sc += qh[i] * (t < pos ? (double)m->kc[loff + (size_t)t * kvd + off + i] : k[off + i]);
+          sc += qh[i] * (t < pos ? (kc64 ? kc64[loff + (size_t)t * kvd + off + i]
+                                         : (double)m->kc[loff + (size_t)t * kvd + off + i])
+                                 : k[off + i]);
         att[t] = sc / sqrt((double)hs);
         if (att[t] > mx) mx = att[t];
       }
@@ -389,7 +428,9 @@ int oracle_forward_f64(OModel* m, int token, int pos, double* logits) {
       for (int t = 0; t <= pos; t++) {
         const double w = att[t] / sum;
         for (int i = 0; i < hs; i++)
-          o[i] += w * (t < pos ? (double)m->vc[loff + (size_t)t * kvd + off + i] : v[off + i]);
+          o[i] += w * (t < pos ? (vc64 ? vc64[loff + (size_t)t * kvd + off + i]
+                                       : (double)m->vc[loff + (size_t)t * kvd + off + i])
+                               : v[off + i]);
       }
     }
     matmul_f64(xb2, xb, m->wo + L * dim * dim, dim, dim);
@@ -404,6 +445,118 @@ int oracle_forward_f64(OModel* m, int token, int pos, double* logits) {
   rmsnorm_f64(xb, x, m->rms_final, dim);
   matmul_f64(logits, xb, m->wcls, dim, p->vocab_size);
   free(x); free(xb); free(xb2); free(q); free(k); free(v); free(hb); free(hb2); free(att);
+  return 0;
+}
+
+/* ------------------------------------------------------------ lockstep batch (fixture generation) */
+/* B independent sequences over ONE copy of the weights, each a view (oracle_model_view_cap) with
+ * its own RunState and K/V cache, stepped together: every per-sequence value is computed exactly
+ * as oracle_forward computes it — each matmul row is the same left-to-right chain from 0.0f, with
+ * no contraction — so views[b]->logits after a call is bit-identical to
+ * oracle_forward(views[b], tokens[b], pos[b]) (tests/test_oracle.py checks it).  Only the loop
+ * nest differs: a tile of 8 rows x 16 sequences walks j once, so the weights are read once per
+ * step instead of once per sequence and 8 independent chains keep the adders busy.  Used to make
+ * the 7B request-workload fixture (tests/golden/make_golden_requests.py). */
+typedef float ov16 __attribute__((vector_size(64)));
+#define OM_R 8  /* rows per tile */
+#define OM_S 16 /* sequences per tile (one ov16) */
+
+__attribute__((target_clones("avx512f", "avx2", "default")))
+static void matmul_tile(float* acc_out, const float* w, const float* xt, int n, int rows) {
+  /* acc_out [OM_R][OM_S]; w rows r < rows of length n; xt [n][OM_S] */
+  ov16 acc[OM_R];
+  for (int r = 0; r < OM_R; r++) acc[r] = (ov16){0};
+  const float* wr[OM_R];
+  for (int r = 0; r < OM_R; r++) wr[r] = w + (size_t)(r < rows ? r : 0) * n;
+  for (int j = 0; j < n; j++) {
+    ov16 xv;
+    memcpy(&xv, xt + (size_t)j * OM_S, sizeof xv);
+    for (int r = 0; r < OM_R; r++) {
+      const ov16 p = wr[r][j] * xv; /* -ffp-contract=off: a separate multiply and add */
+      acc[r] = acc[r] + p;
+    }
+  }
+  memcpy(acc_out, acc, sizeof acc);
+}
+
+/* xout[b][i] = sum_j w[i][j] * x[b][j], i < d, in seq.cpp:40-51's order for every b */
+static void matmul_multi(float* const* xout, float* const* x, const float* w, int n, int d, int B, float* xt) {
+  for (int s0 = 0; s0 < B; s0 += OM_S) {
+    const int ns = B - s0 < OM_S ? B - s0 : OM_S;
+    for (int j = 0; j < n; j++)
+      for (int s = 0; s < OM_S; s++) xt[(size_t)j * OM_S + s] = s < ns ? x[s0 + s][j] : 0.0f;
+    const int tiles = (d + OM_R - 1) / OM_R;
+    int t;
+#pragma omp parallel for num_threads(g_threads) if (g_threads > 1) schedule(dynamic, 4)
+    for (t = 0; t < tiles; t++) {
+      const int i0 = t * OM_R, rows = d - i0 < OM_R ? d - i0 : OM_R;
+      float acc[OM_R][OM_S];
+      matmul_tile(&acc[0][0], w + (size_t)i0 * n, xt, n, rows);
+      for (int r = 0; r < rows; r++)
+        for (int s = 0; s < ns; s++) xout[s0 + s][i0 + r] = acc[r][s];
+    }
+  }
+}
+
+OModel* oracle_model_view_cap(OModel* m, int seq_cap);
+
+int oracle_forward_multi(OModel** ms, int B, const int* tokens, const int* pos) {
+  if (B <= 0) return 0;
+  const OCfg* p = &ms[0]->c;
+  const int dim = p->dim, hid = p->hidden_dim, hs = dim / p->n_heads;
+  const int kvd = (p->dim * p->n_kv_heads) / p->n_heads, kv_mul = p->n_heads / p->n_kv_heads;
+  for (int b = 0; b < B; b++)
+    if (pos[b] < 0 || pos[b] >= ms[b]->c.seq_len || ms[b]->emb != ms[0]->emb) return -1;
+  float** in = malloc(sizeof(float*) * B);
+  float** out = malloc(sizeof(float*) * B);
+  float** out2 = malloc(sizeof(float*) * B);
+  float* xt = malloc(sizeof(float) * (size_t)(hid > dim ? hid : dim) * OM_S);
+  if (!in || !out || !out2 || !xt) { free(in); free(out); free(out2); free(xt); return -1; }
+  const OModel* w = ms[0];
+  int b;
+#pragma omp parallel for num_threads(g_threads) if (g_threads > 1)
+  for (b = 0; b < B; b++) memcpy(ms[b]->x, w->emb + (size_t)tokens[b] * dim, dim * sizeof(float));
+  for (unsigned long long l = 0; l < (unsigned long long)p->n_layers; l++) {
+#pragma omp parallel for num_threads(g_threads) if (g_threads > 1)
+    for (b = 0; b < B; b++) oracle_rmsnorm(ms[b]->xb, ms[b]->x, w->rms_att + l * dim, dim);
+    for (b = 0; b < B; b++) in[b] = ms[b]->xb, out[b] = ms[b]->q;
+    matmul_multi(out, in, w->wq + l * dim * dim, dim, dim, B, xt);
+    for (b = 0; b < B; b++) out[b] = ms[b]->kc + l * ms[b]->c.seq_len * (size_t)kvd + (size_t)pos[b] * kvd;
+    matmul_multi(out, in, w->wk + l * dim * kvd, dim, kvd, B, xt);
+    for (b = 0; b < B; b++) out2[b] = ms[b]->vc + l * ms[b]->c.seq_len * (size_t)kvd + (size_t)pos[b] * kvd;
+    matmul_multi(out2, in, w->wv + l * dim * kvd, dim, kvd, B, xt);
+#pragma omp parallel for num_threads(g_threads) if (g_threads > 1) schedule(dynamic, 1)
+    for (b = 0; b < B; b++) {
+      OModel* m = ms[b];
+      const size_t loff = l * m->c.seq_len * (size_t)kvd;
+      oracle_rope(m->q, m->kc + loff + (size_t)pos[b] * kvd, dim, hs, kvd, pos[b]);
+      oracle_attention(m->xb, m->att, m->q, m->kc + loff, m->vc + loff, pos[b], p->n_heads, hs, kvd, kv_mul,
+                       m->c.seq_len);
+    }
+    for (b = 0; b < B; b++) out[b] = ms[b]->xb2;
+    matmul_multi(out, in, w->wo + l * dim * dim, dim, dim, B, xt);
+#pragma omp parallel for num_threads(g_threads) if (g_threads > 1)
+    for (b = 0; b < B; b++) {
+      OModel* m = ms[b];
+      for (int i = 0; i < dim; i++) m->x[i] += m->xb2[i];
+      oracle_rmsnorm(m->xb, m->x, w->rms_ffn + l * dim, dim);
+    }
+    for (b = 0; b < B; b++) out[b] = ms[b]->hb, out2[b] = ms[b]->hb2;
+    matmul_multi(out, in, w->w1 + l * dim * hid, dim, hid, B, xt);
+    matmul_multi(out2, in, w->w3 + l * dim * hid, dim, hid, B, xt);
+#pragma omp parallel for num_threads(g_threads) if (g_threads > 1)
+    for (b = 0; b < B; b++) oracle_swiglu(ms[b]->hb, ms[b]->hb2, hid);
+    for (b = 0; b < B; b++) in[b] = ms[b]->hb, out[b] = ms[b]->xb;
+    matmul_multi(out, in, w->w2 + l * dim * hid, hid, dim, B, xt);
+#pragma omp parallel for num_threads(g_threads) if (g_threads > 1)
+    for (b = 0; b < B; b++)
+      for (int i = 0; i < dim; i++) ms[b]->x[i] += ms[b]->xb[i];
+  }
+#pragma omp parallel for num_threads(g_threads) if (g_threads > 1)
+  for (b = 0; b < B; b++) oracle_rmsnorm(ms[b]->x, ms[b]->x, w->rms_final, dim);
+  for (b = 0; b < B; b++) in[b] = ms[b]->x, out[b] = ms[b]->logits;
+  matmul_multi(out, in, w->wcls, dim, p->vocab_size, B, xt);
+  free(in); free(out); free(out2); free(xt);
   return 0;
 }
 
@@ -629,12 +782,19 @@ int oracle_q8_greedy(OModel* m, int token, int pos0, int n, int* out) {
 /* BASELINE.md CPU-baseline plan (ii): P independent single-threaded decoders, one per core, over
  * disjoint sequences (decoder i starts from token 1 + i at pos 0), sharing one copy of the
  * weights; each is the unchanged single-sequence forward above with its own RunState. */
-OModel* oracle_model_view(OModel* m) {
+OModel* oracle_model_view(OModel* m) { return oracle_model_view_cap(m, 0); }
+
+/* A view whose K/V cache holds positions 0..seq_cap-1 only (seq_cap <= 0: the model's seq_len).
+ * The cache stride is the only thing seq_len sets in the forward (RoPE and attention read
+ * positions 0..pos), so a capped view computes the same values for every pos < seq_cap. */
+OModel* oracle_model_view_cap(OModel* m, int seq_cap) {
   OModel* v = calloc(1, sizeof(OModel));
   if (!v) return NULL;
   *v = *m; /* weight pointers */
+  if (seq_cap > 0 && seq_cap < v->c.seq_len) v->c.seq_len = seq_cap;
   v->view = 1;
   v->x = v->xb = v->xb2 = v->hb = v->hb2 = v->q = v->att = v->logits = v->kc = v->vc = v->k = v->v = NULL;
+  v->kc64 = v->vc64 = NULL;
   v->xq.q = v->hq.q = NULL;
   v->xq.s = v->hq.s = NULL;
   if (!alloc_state(v)) { oracle_model_free(v); return NULL; }

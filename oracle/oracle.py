@@ -67,6 +67,7 @@ def lib():
             "oracle_model_free": (None, [V]),
             "oracle_forward": (F, [V, C.c_int, C.c_int]),
             "oracle_forward_f64": (C.c_int, [V, C.c_int, C.c_int, C.POINTER(C.c_double)]),
+            "oracle_forward_f64_ex": (C.c_int, [V, C.c_int, C.c_int, C.POINTER(C.c_double), C.c_int]),
             "oracle_argmax": (C.c_int, [F, C.c_int]),
             "oracle_greedy": (C.c_int, [V, C.c_int, C.c_int, C.c_int, IP]),
             "oracle_q8_quantize": (None, [I8, F, F, C.c_int, C.c_int]),
@@ -80,6 +81,8 @@ def lib():
             "oracle_q8_greedy": (C.c_int, [V, C.c_int, C.c_int, C.c_int, IP]),
             "oracle_synth_fill": (None, [F, S, U64, C.c_int, C.c_double, S]),
             "oracle_aggregate": (C.c_double, [V, C.c_int, C.c_int, IP, C.c_int, C.c_int, IP]),
+            "oracle_model_view_cap": (V, [V, C.c_int]),
+            "oracle_forward_multi": (C.c_int, [C.POINTER(V), C.c_int, IP, IP]),
         }
         for n, (r, a) in sig.items():
             fn = getattr(L, n)
@@ -197,11 +200,15 @@ class Model:
         p = lib().oracle_forward(self.h, token, pos)
         return np.ctypeslib.as_array(p, shape=(self.vocab,)).copy()
 
-    def forward_f64(self, token, pos):
-        """The same forward in double precision from this model's K/V rows 0..pos-1 (the cache is
-        not modified): the exact value of the reference's arithmetic, to attribute rounding."""
+    def forward_f64(self, token, pos, rope_double=False, own_cache=False):
+        """The same forward in double precision from this model's K/V rows 0..pos-1 (the fp32 cache
+        is not modified): the exact value of the reference's arithmetic, to attribute rounding.
+        rope_double: RoPE's (cos, sin) in double too (default: the reference's float values);
+        own_cache: earlier positions' K/V from this function's own double cache (written by every
+        own_cache call) instead of the fp32 cache — with both, src/seq.cpp widened to double."""
         out = np.zeros(self.vocab, np.float64)
-        if lib().oracle_forward_f64(self.h, token, pos, out.ctypes.data_as(C.POINTER(C.c_double))) != 0:
+        flags = (1 if rope_double else 0) | (2 if own_cache else 0)
+        if lib().oracle_forward_f64_ex(self.h, token, pos, out.ctypes.data_as(C.POINTER(C.c_double)), flags) != 0:
             raise MemoryError("oracle_forward_f64")
         return out
 
@@ -277,6 +284,42 @@ class Model:
             pass
 
 
+class Lockstep:
+    """B sequences over one Model's weights, stepped together (oracle_forward_multi): each
+    sequence has its own RunState and K/V cache (positions < seq_cap), and its logits are
+    bit-identical to Model.forward's for the same (token, pos) history.  Fixture generation."""
+
+    def __init__(self, model, B, seq_cap=0):
+        self.model, self.vocab = model, model.vocab
+        self.views = [lib().oracle_model_view_cap(model.h, int(seq_cap)) for _ in range(B)]
+        if not all(self.views):
+            self.close()
+            raise MemoryError("oracle_model_view_cap")
+
+    def forward(self, idx, tokens, pos):
+        """One step of the sequences idx (indices into this batch) at (tokens, pos): logits [len(idx)][V]."""
+        n = len(idx)
+        arr = (C.c_void_p * n)(*[self.views[i] for i in idx])
+        tk = (C.c_int * n)(*[int(t) for t in tokens])
+        ps = (C.c_int * n)(*[int(p) for p in pos])
+        if lib().oracle_forward_multi(arr, n, tk, ps) != 0:
+            raise ValueError("oracle_forward_multi: bad position or mixed models")
+        return np.stack([np.ctypeslib.as_array(lib().oracle_model_logits(self.views[i]), shape=(self.vocab,)).copy()
+                         for i in idx]) if n else np.zeros((0, self.vocab), np.float32)
+
+    def close(self):
+        for v in getattr(self, "views", []):
+            if v:
+                lib().oracle_model_free(v)
+        self.views = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 # ---------------------------------------------------------------- the reference itself (oracle/_ref)
 def have_ref():
     return os.path.exists(REF_SEQ)
@@ -310,6 +353,26 @@ def ref_q8_lib():
         L.ref_q8_greedy.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, IP, F]
         _refq = L
     return _refq
+
+
+REF_SEQ_F64 = os.path.join(HERE, "_ref", "libref_seq_f64.so")
+
+
+def have_ref_f64():
+    return os.path.exists(REF_SEQ_F64)
+
+
+def ref64_forced(path, tokens, vocab):
+    """The reference's src/seq.cpp widened to double (oracle/ref_f64_driver.cpp): teacher-forced
+    logits [n][vocab] (float64) of tokens[i] at position i."""
+    L = C.CDLL(REF_SEQ_F64)
+    L.ref64_forced.argtypes = [C.c_char_p, IP, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    n = len(tokens)
+    out = np.zeros(n * vocab, np.float64)
+    if L.ref64_forced(path.encode(), (C.c_int * n)(*[int(t) for t in tokens]), 0, n,
+                      out.ctypes.data_as(C.POINTER(C.c_double))) != 0:
+        raise IOError(path)
+    return out.reshape(n, vocab)
 
 
 def ref_greedy(path, token, pos0, n, vocab):

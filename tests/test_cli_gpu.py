@@ -108,6 +108,31 @@ def test_test_mode_worker_split_replicas(gpu, host, model, tmp_path, batch):
     assert f"Total achieved token: {gen}".encode() in r.stdout
 
 
+@pytest.mark.parametrize("path", ["rccl", "peer", "upload"])
+def test_test_mode_replication_paths(gpu, host, model, tmp_path, path):
+    """Every way the CLI can fill a second replica (app/run.cpp replicate), on this one GPU with
+    THALLAMA_REPLICAS=2: `peer` (hipMemcpyPeer), `upload` (the reference's per-GPU upload from the
+    host image), and `rccl` forced over two replicas of ONE device — ncclCommInitAll rejects the
+    duplicate device, which is exactly a failing RCCL: the run must report it, fall back to peer
+    copies and still write the single-worker output file."""
+    ref, path_ = model
+    inp = tmp_path / "in.txt"
+    inp.write_bytes((f"{len(PROMPTS)}\n" + "\n".join(PROMPTS) + "\n").encode())
+    out = tmp_path / "out.txt"
+    r = run_cli([path_, "-m", "test", "-f", str(inp), "-o", str(out), "-b", "2", "-z", TOK], tmp_path,
+                env={"THALLAMA_REPLICAS": "2", "THALLAMA_REPLICATE": path})
+    so = r.stdout.decode()
+    if path == "rccl":
+        assert "replication: RCCL failed" in so and "falling back to peer copies" in so, so[-2000:]
+        assert "replication: peer to 2 replica(s)" in so
+    else:
+        assert f"replication: {path} to 2 replica(s) on 1 GPU(s)" in so
+    assert sum(1 for ln in so.splitlines() if ln.startswith("worker ") and " cpu " in ln) == 2
+    want, gen = expected_test_mode(host, ref, PROMPTS, CFG[6])
+    assert out.read_bytes() == f"{len(PROMPTS)}\n".encode() + b"".join(w + b"\n" for w in want)
+    assert f"Total achieved token: {gen}".encode() in r.stdout
+
+
 def test_test_mode_rccl_broadcast_multi_device(gpu, host, model, tmp_path):
     """With more than one visible device the CLI uploads the weights once and fans them out with
     RCCL (app/run.cpp replicate: ncclCommInitAll + ncclBroadcast in 1-GiB pieces; reference
@@ -123,7 +148,7 @@ def test_test_mode_rccl_broadcast_multi_device(gpu, host, model, tmp_path):
     out = tmp_path / "out.txt"
     r = run_cli([path, "-m", "test", "-f", str(inp), "-o", str(out), "-b", "2", "-z", TOK], tmp_path)
     assert f"Num Devices {n_dev}".encode() in r.stderr
-    assert f"RCCL broadcast to {n_dev} GPUs".encode() in r.stdout
+    assert f"replication: rccl to {n_dev} replica(s) on {n_dev} GPU(s)".encode() in r.stdout
     want, gen = expected_test_mode(host, ref, PROMPTS, CFG[6])
     assert out.read_bytes() == f"{len(PROMPTS)}\n".encode() + b"".join(w + b"\n" for w in want)
     assert f"Total achieved token: {gen}".encode() in r.stdout

@@ -130,3 +130,55 @@ def test_reference_cli_on_the_library_test_mode(gpu, oracle, pkg, tmp_path, batc
     assert r.returncode == 0, r.stderr.decode()[-2000:]
     want, _ = T.expected_test_mode(H, ref, T.PROMPTS, T.CFG[6])
     assert out.read_bytes() == f"{len(T.PROMPTS)}\n".encode() + b"".join(w + b"\n" for w in want)
+
+
+@pytest.mark.gpu
+def test_reference_cli_timed_beside_ours(gpu, oracle, pkg, tmp_path):
+    """The drop-in's cost as the reference's own driver uses it: its UNCHANGED src/llama.cpp test
+    mode on libthallama.so — per step an H2D of token/pos, thaDNN_s_forward_batch, a D2H of the
+    B x V logits, a device synchronisation and host sampling (src/thaDNN.cpp:24-79,
+    src/llama.cpp:1024-1050) — timed beside this repository's CLI (build/apps/llama, the same
+    sampling) on the same stories110M-shaped v0 file and the first 16 prompts of the reference's
+    gen_in_128.txt, each request to seq_len 1024 or BOS/EOS, 8 slots.  The classifier is scaled
+    (peaked distributions) so both samplers draw the same tokens from logits within 1e-4: the two
+    output files must be equal.  Both throughputs (the reference's own "achieved throughput" line)
+    go to gpurun_out/dropin_timing.json."""
+    import json
+    import time
+    if not os.path.exists(BUILT):
+        pytest.skip("oracle/_ref/llama_on_thallama not built (needs the reference tree at build time)")
+    cfg = (768, 2048, 12, 12, 12, 32000, 1024)
+    base = oracle.Model(cfg, 0, seed=110)
+    arena = base.arena().copy()
+    arena[-cfg[5] * cfg[0]:] *= 30.0
+    path = str(tmp_path / "stories110m_peaked.bin")
+    oracle.Model(cfg, 0, payload=arena).write_v0(path)
+    with open(os.path.join(REPO, "tests", "golden", "gen_in_128.txt"), "rb") as f:
+        lines = f.read().split(b"\n")
+    n = 16
+    inp = tmp_path / "in.txt"
+    inp.write_bytes(f"{n}\n".encode() + b"\n".join(lines[1:1 + n]) + b"\n")
+    shutil.copy(os.path.join(REPO, "tests", "golden", "tokenizer.bin"), tmp_path / "tokenizer.bin")
+    res = {}
+    outs = {}
+    for name, exe in (("reference_cli_on_libthallama", BUILT), ("this_cli", os.path.join(REPO, "build", "apps", "llama"))):
+        out = tmp_path / f"out_{name}.txt"
+        t0 = time.perf_counter()
+        r = subprocess.run([exe, path, "-m", "test", "-f", str(inp), "-o", str(out), "-b", "8", "-z",
+                            str(tmp_path / "tokenizer.bin")], cwd=tmp_path, capture_output=True, text=True, timeout=600)
+        wall = time.perf_counter() - t0
+        assert r.returncode == 0, r.stderr[-2000:]
+        tot = [ln for ln in r.stdout.splitlines() if ln.startswith("Total achieved token:")]
+        el = [ln for ln in r.stdout.splitlines() if ln.startswith("elapsed time(s):")]
+        tokens, secs = int(tot[-1].split()[-1]), float(el[-1].split()[2].rstrip(","))
+        res[name] = {"tokens": tokens, "seconds": secs, "tok_s": round(tokens / secs, 1), "wall_s": round(wall, 2)}
+        outs[name] = out.read_bytes()
+    res["outputs_equal"] = outs["reference_cli_on_libthallama"] == outs["this_cli"]
+    res["workload"] = (f"stories110M-shaped fp32 v0 file (classifier x30), first {n} prompts of gen_in_128.txt, -m test "
+                       "-b 8 (T=1.0, top-p 0.9, seed 314028 per request), each request to seq_len 1024 or BOS/EOS")
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", "dropin_timing.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res))
+    assert res["outputs_equal"]
+    assert res["reference_cli_on_libthallama"]["tokens"] == res["this_cli"]["tokens"]

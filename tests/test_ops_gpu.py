@@ -157,7 +157,7 @@ def test_matmul_batch_offsets(gpu, handle, oracle, B):
 def test_matmul_batch_register_resident(gpu, handle, oracle, M, K, B):
     """Batched GEMV at 7B row counts: B = 4 takes the register-resident kernel (gemv_rr.hpp; K =
     11008 is three passes of 16 / 16 / 11 chunks, the last pass leaves waves idle), B = 5 and 8 the
-    matrix-core kernel (the register-resident one with THALLAMA_GEMV_RR=8); 1e-4 vs the oracle."""
+    matrix-core kernel; 1e-4 vs the oracle."""
     r = rng(M + K + B)
     W = (r.standard_normal((M, K)) * 0.02).astype(np.float32)
     X = r.standard_normal((B, K)).astype(np.float32)

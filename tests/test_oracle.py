@@ -88,6 +88,66 @@ def test_oracle_thread_count_invariant(oracle):
     np.testing.assert_array_equal(outs[0], outs[1])
 
 
+@pytest.mark.skipif(not os.path.exists(os.path.join(os.path.dirname(HERE), "oracle", "_ref", "libref_seq_f64.so")),
+                    reason="reference build oracle/_ref absent")
+@pytest.mark.parametrize("cfg,shared", [((768, 2048, 2, 12, 12, 32000, 64), 0),   # stories110M-shaped layers
+                                        ((128, 384, 2, 8, 4, 700, 48), 1),        # GQA, shared classifier
+                                        ((128, 384, 3, 8, 2, 700, 48), 0)])       # kv_mul 4
+def test_forward_f64_matches_widened_reference(oracle, tmp_path, cfg, shared):
+    """oracle_forward_f64 — the 'exact' forward the GPU's and the CPU's logits are measured against
+    (tests/test_golden_2048_gpu.py) — pinned to the reference itself: its src/seq.cpp compiled with
+    float widened to double (oracle/ref_f64_driver.cpp, read in place) gives BIT-IDENTICAL logits at
+    every position of a teacher-forced run when forward_f64 also computes RoPE's (cos, sin) in double
+    and keeps its own double K/V rows.  Its default mode differs from that only by taking the
+    reference's float RoPE parameters and the caller's fp32 K/V rows, both inputs rather than
+    accumulations; at this size that moves logits by less than the fp32 forward's own rounding."""
+    m = oracle.Model(cfg, shared, seed=11)
+    path = str(tmp_path / "m.bin")
+    m.write_v0(path)
+    V = abs(cfg[5])
+    toks = [int(t) for t in np.random.default_rng(cfg[2]).integers(0, V, 14)]
+    ref = oracle.ref64_forced(path, toks, V)
+    worst_default, worst_fp32 = 0.0, 0.0
+    for p, t in enumerate(toks):
+        np.testing.assert_array_equal(m.forward_f64(t, p, rope_double=True, own_cache=True), ref[p],
+                                      err_msg=f"position {p}")
+        dflt = m.forward_f64(t, p)  # (reads the fp32 cache rows of the fp32 forwards before it)
+        fp32 = m.forward(t, p).astype(np.float64)
+        worst_default = max(worst_default, float(np.abs(dflt - ref[p]).max()))
+        worst_fp32 = max(worst_fp32, float(np.abs(fp32 - ref[p]).max()))
+    assert worst_default < worst_fp32, (worst_default, worst_fp32)
+
+
+def test_lockstep_matches_single_forward(oracle):
+    """oracle_forward_multi (the fixture generator of make_golden_requests.py) is bit-identical to
+    the single-sequence forward: 21 sequences (two 16-sequence tiles), GQA, row counts that end
+    mid-tile, sequences entering at different steps (ragged positions in one call), a capped cache."""
+    cfg = (120, 332, 2, 6, 3, 251, 48)
+    B, steps = 21, 14
+    oracle.set_threads(4)
+    base = oracle.Model(cfg, 0, seed=41)
+    ls = oracle.Lockstep(base, B, seq_cap=steps)
+    rng = np.random.default_rng(5)
+    toks = rng.integers(0, cfg[5], size=(B, steps))
+    start = [b % 4 for b in range(B)]  # sequence b enters at step start[b]
+    singles = [oracle.Model(cfg, 0, seed=41) for _ in range(3)]  # one reference model reused per b
+    want = {}
+    for b in range(B):
+        m = singles[b % 3]
+        m.reset_kv()
+        for p in range(steps - start[b]):
+            want[(b, p)] = m.forward(int(toks[b, p]), p)
+    for s in range(steps):
+        idx = [b for b in range(B) if s >= start[b]]
+        pos = [s - start[b] for b in idx]
+        lg = ls.forward(idx, [toks[b, p] for b, p in zip(idx, pos)], pos)
+        for r, (b, p) in enumerate(zip(idx, pos)):
+            np.testing.assert_array_equal(lg[r], want[(b, p)], err_msg=f"sequence {b} position {p}")
+    oracle.set_threads(1)
+    with pytest.raises(ValueError):
+        ls.forward([0], [1], [steps])  # past the capped cache
+
+
 def test_ops_known_answers(oracle):
     # rmsnorm of a constant vector is the weight (ss = 1/|c|): x=2 -> 1/sqrt(4+1e-5)*2
     x = np.full(16, 2.0, np.float32)

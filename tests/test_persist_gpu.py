@@ -115,6 +115,33 @@ def test_cooperative_launch(gpu):
         assert gpu.lib().thallama_persistent_cooperative() == 1
 
 
+def test_plain_launch_switch(gpu):
+    """THALLAMA_PERSIST_COOP=0 — the one launch switch left, for rocprofv3 runs (the profiler fails
+    at exit after a cooperative launch, tools/prof_r04.sh) — gives a plain launch of the same grid
+    and the same greedy tokens as the CPU oracle (a fresh process: the choice is made once)."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+        "from __graft_entry__ import _pkg; _pkg()\n"
+        "from hip_llama_cpp_amd import thallama as tl\n"
+        "import oracle as O\n"
+        "tl.check(tl.lib().thallama_set_device(0))\n"
+        "cfg = (256, 768, 2, 4, 2, 1024, 128)\n"
+        "c = tl.Config.make(*cfg); m = tl.DeviceModel(c, 0, seed=5); st = tl.DeviceState(c, 1)\n"
+        "d = tl.Decoder(m, st); assert d.persistent()\n"
+        "got = d.greedy([1], [0], 24)[:, 0].tolist()\n"
+        "want = O.Model(cfg, 0, seed=5).greedy(1, 0, 24)\n"
+        "assert tl.lib().thallama_persistent_cooperative() == 0\n"
+        "assert d.persistent() and got == want, (got, want)\n"
+        "print('plain launch OK')\n") % (repo, os.path.join(repo, "oracle"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env={**os.environ, "THALLAMA_PERSIST_COOP": "0"})
+    assert r.returncode == 0 and "plain launch OK" in r.stdout, r.stderr[-3000:]
+
+
 @pytest.mark.parametrize("cfg", [SMALL, HEAD128, RAGGED])
 def test_forced_logits_every_step(gpu, oracle, cfg):
     _, _, _, dec = decoder(gpu, cfg, 0, 9, 1)

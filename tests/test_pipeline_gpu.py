@@ -135,3 +135,80 @@ def test_forward_70B_layer_streaming_matches_oracle(gpu, oracle, shared):
     tl.lib().thallama_forward_batch_cache_clear()
     L.free_weight_device(d_w)
     tl.lib().free_state_device(d_s)
+
+
+def test_pipeline_four_threads_cache_follows_working_set(gpu, oracle):
+    """The reference's test_pipeline_parallelism drives the pipeline from 4 host threads, each with
+    its own handle per device (src/llama.cpp:1298): 4 threads x 4 stages = 16 stage decoders, twice
+    the decoder cache's starting size.  The cache must grow to that working set (thrashing would
+    re-create a decoder — workspaces, RoPE table — on every call): after the first rounds the
+    number of live decoders stays flat, and every thread's logits stay the oracle's."""
+    import threading
+    tl = gpu
+    cfg, shared, seed, B, n_stages, n_threads = CFG, 0, 45, 1, 4, 4
+    base = oracle.Model(cfg, shared, seed=seed)
+    arena = base.arena().copy()
+    t_h = host_transformer(tl, cfg, arena, shared)
+    c = tl.Config.make(*cfg)
+    L = tl.lib()
+    L.thallama_forward_batch_cache_clear()
+    pipe = cfg[2] // n_stages
+    wps = (C.POINTER(tl.TransformerWeights) * n_stages)()
+    for g in range(n_stages):
+        wp = C.POINTER(tl.TransformerWeights)()
+        L.copy_transformer_weight_pipeline_to_device_batch(C.byref(t_h), C.byref(wp), pipe, g, B)
+        wps[g] = wp
+    per = []
+    for t in range(n_threads):
+        hs = handles(tl, n_stages)
+        sps = (C.POINTER(tl.RunState) * n_stages)()
+        for g in range(n_stages):
+            sp = C.POINTER(tl.RunState)()
+            L.alloc_run_state_to_device_batch(hs[g], C.byref(t_h), C.byref(sp), pipe, g, B)
+            sps[g] = sp
+        per.append((hs, sps))
+    steps = 12
+    toks = [[(7 * t + 3 * p) % cfg[5] for p in range(steps)] for t in range(n_threads)]
+    got = [[None] * steps for _ in range(n_threads)]
+    live = [[0] * steps for _ in range(n_threads)]
+    errs = []
+    start = threading.Barrier(n_threads)
+
+    def worker(t):
+        try:
+            hs, sps = per[t]
+            start.wait()
+            lg = np.zeros(cfg[5], np.float32)
+            for p in range(steps):
+                rc = L.thaDNN_s_forward_batch_multiple_pipe_line(hs, 0, 1, n_stages, B, C.byref(c), wps, sps,
+                                                                 (C.c_int * 1)(toks[t][p]), (C.c_int * 1)(p),
+                                                                 lg.ctypes.data_as(tl.c_float_p), None, None, None)
+                assert rc == 0, (t, p, L.thallama_last_error())
+                got[t][p] = lg.copy()
+                live[t][p] = L.thallama_forward_batch_live()
+        except BaseException as e:  # noqa: BLE001 - reported below
+            errs.append(e)
+
+    ts = [threading.Thread(target=worker, args=(t,)) for t in range(n_threads)]
+    for th in ts:
+        th.start()
+    for th in ts:
+        th.join(timeout=300)
+    assert not any(th.is_alive() for th in ts), "a worker thread did not finish"
+    if errs:
+        raise errs[0]
+    cap = L.thallama_forward_batch_cache_cap()
+    assert cap >= n_threads * n_stages, cap
+    assert L.thallama_forward_batch_cache_size() == n_threads * n_stages
+    tail = {live[t][p] for t in range(n_threads) for p in range(steps // 2, steps)}
+    assert tail == {n_threads * n_stages}, (tail, live)
+    for t in range(n_threads):
+        ref = oracle.Model(cfg, shared, seed=seed)
+        for p in range(steps):
+            assert_ref_close(got[t][p], ref.forward(toks[t][p], p), 1e-4, f"thread {t} pos {p}")
+    L.thallama_forward_batch_cache_clear()
+    for t in range(n_threads):
+        for g in range(n_stages):
+            L.free_state_device(per[t][1][g])
+    for g in range(n_stages):
+        L.free_weight_device(wps[g])

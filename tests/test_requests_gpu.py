@@ -1,0 +1,85 @@
+"""BASELINE.json configs[4]'s per-GPU workload on the GPU, against a fixture the CPU wrote: the drop-in
+CLI (build/apps/llama, app/run.cpp — the reference's test_data_parallelism, src/llama.cpp:891-1083)
+in greedy test mode over the reference's gen_in_64.txt prompts on the llama2-7B synthetic model the
+bench uses, each request to position 255 or BOS/EOS (THALLAMA_TEST_STEPS=256), compared with
+tests/golden/requests_llama2-7B_f32_gen_in_64.json — made by tests/golden/make_golden_requests.py with
+the oracle's lockstep forward (bit-identical to the reference's src/seq.cpp; its BOS sequence checked
+against the reference's own 256 tokens).  Distinct prompts at distinct positions in one batch at 7B.
+
+A request's output must equal the fixture's byte for byte, except a request that reaches a near-tie
+of the CPU reference (top-2 margin < 1e-4) and takes the other branch there (bench.compare_request_file,
+the rule of tests/test_cli_gpu.py::test_gen_in_128_greedy_fixture); which requests did is printed and
+written under gpurun_out/.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+
+EXE = os.path.join(REPO, "build", "apps", "llama")
+TOK = os.path.join(REPO, "tests", "golden", "tokenizer.bin")
+FIXTURE = os.path.join(REPO, "tests", "golden", "requests_llama2-7B_f32_gen_in_64.json")
+SPEC = "synth:4096,11008,32,32,32,-32000,2048:20240224"
+
+
+@pytest.fixture(scope="module")
+def fixture():
+    with open(FIXTURE) as f:
+        fx = json.load(f)
+    assert fx["generator"].startswith("tests/golden/make_golden_requests.py")
+    assert fx["decode_len"] == 256 and fx["seed"] == bench.SEED and fx["bos_check"]["tokens_match"]
+    return fx
+
+
+def run_cli(tmp_path, n, batch, env=None):
+    assert os.path.exists(EXE), "build the CLI: make -C hip_llama.cpp_amd"
+    with open(os.path.join(REPO, "tests", "golden", "gen_in_64.txt"), "rb") as f:
+        lines = f.read().split(b"\n")
+    inp = tmp_path / "in.txt"
+    inp.write_bytes(f"{n}\n".encode() + b"\n".join(lines[1:1 + n]) + b"\n")
+    out = tmp_path / "out.txt"
+    e = {**os.environ, "THALLAMA_TEST_STEPS": "256", **(env or {})}
+    r = subprocess.run([EXE, SPEC, "-m", "test", "-f", str(inp), "-o", str(out), "-b", str(batch), "-g", "1",
+                        "-z", TOK], cwd=REPO, capture_output=True, timeout=600, env=e)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    return out.read_bytes(), r.stdout.decode()
+
+
+def check(fx, got, stdout, n, tag):
+    res = bench.compare_request_file(got, fx, n)
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", f"requests_7b_{tag}.json"), "w") as f:
+        json.dump(res, f)
+    print(f"{tag}: identical {res['identical']}, diverged (request, position, top-2 margin) {res['diverged']}")
+    assert not res["unexplained"], res
+    assert res["ok"], res
+    if res["identical"]:
+        assert f"Total achieved token: {sum(fx['achieved_tokens'][:n])}" in stdout
+    return res
+
+
+@pytest.mark.parametrize("batch,n", [(8, 64), (1, 16)])
+def test_gen_in_64_7b_matches_oracle_fixture(gpu, fixture, tmp_path, batch, n):
+    """-b 8: all 64 prompts through the batched step (8 distinct prompts at their own positions per
+    step, prompts prefilled); -b 1: the first 16 through the persistent one-sequence step."""
+    got, out = run_cli(tmp_path, n, batch)
+    check(fixture, got, out, n, f"b{batch}_n{n}")
+
+
+def test_gen_in_64_7b_two_replicas_no_rccl(gpu, fixture, tmp_path):
+    """The N-GPU worker split rehearsed on one GPU: two workers and replicas, the second replica's
+    weights by the fall-back peer copy (THALLAMA_REPLICATE=peer, no RCCL); 16 prompts at 8 slots
+    per worker.  The file equals the fixture, and the per-worker lines cover every request."""
+    got, out = run_cli(tmp_path, 16, 8, env={"THALLAMA_REPLICAS": "2", "THALLAMA_REPLICATE": "peer"})
+    assert "replication: peer to 2 replica(s) on 1 GPU(s)" in out
+    check(fixture, got, out, 16, "replicas2_peer")
+    reqs = [int(ln.split()[9]) for ln in out.splitlines() if ln.startswith("pass 0 worker ")]
+    assert len(reqs) == 2 and sum(reqs) == 16
