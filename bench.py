@@ -73,14 +73,21 @@ def fixture_path(mname, dtype, T):
     return p if fx.get("decode_len") == T and fx.get("seed") == SEED else None
 
 
-def compare_request_file(got, fx, n, tie_margin=1e-4):
+# llama2-7B fp32: the GPU's teacher-forced logits drift up to 1.75e-4 from the CPU reference's over a
+# 2048-step decode (profiles/r03/drift_2048_7b_fp32.json; the reference's own GPU path: 5.35e-4,
+# tests/golden/reference_gpu_drift_2048.json), so a greedy step whose top-2 margin is under 2e-4 may
+# go either way on any fp32 path with another summation order than src/seq.cpp's
+REQUEST_TIE_7B = 2e-4
+
+
+def compare_request_file(got, fx, n, tie_margin=1e-4, tight=1e-5):
     """The CLI's output file for the first n requests against the fixture.  Byte-identical, or else
     every request's record equals the fixture's except a request whose greedy decode reaches a
     near-tie of the CPU reference (top-2 logit margin < tie_margin: fp32 summation order alone can
     flip it) and leaves the fixture's text within that step's piece; the rest of such a request is
     unpinned.  Returns {"identical", "diverged": [[request, position, margin]], "unexplained": [...],
     "ok"}; ok allows at most as many diverged requests as the fixture has requests with a tie under
-    1e-5 (tests/test_requests_gpu.py, the same rule as tests/test_cli_gpu.py)."""
+    `tight` (tests/test_requests_gpu.py; tests/test_cli_gpu.py applies the same rule at 110M)."""
     ws = [o.encode("latin-1") + b"\n" for o in fx["outputs"][:n]]  # a record: output + "\n"
     head = f"{n}\n".encode()
     res = {"identical": got == head + b"".join(ws), "requests": n, "diverged": [], "unexplained": []}
@@ -114,7 +121,7 @@ def compare_request_file(got, fx, n, tie_margin=1e-4):
                 rest = b""
         if rest:
             res["unexplained"].append("trailing bytes")
-    n_tight = sum(1 for ts in fx["near_ties"][:n] if any(t[1] < 1e-5 for t in ts))
+    n_tight = sum(1 for ts in fx["near_ties"][:n] if any(t[1] < tight for t in ts))
     res["ok"] = res["identical"] or (not res["unexplained"] and len(res["diverged"]) <= n_tight)
     return res
 
@@ -156,6 +163,8 @@ def parse_args(argv):
     ap.add_argument("--splits", type=int, default=0)
     ap.add_argument("--no-persistent", action="store_true",
                     help="multi-launch step instead of the one-launch persistent step")
+    ap.add_argument("--no-fuse", action="store_true",
+                    help="batch 5..8: attention and Wo as two launches instead of one (attn_wo.hip)")
     ap.add_argument("--no-long", action="store_true", help="skip the positions 1792..2047 line")
     ap.add_argument("--no-requests-point", action="store_true", help="skip the 1-GPU request-workload point")
     ap.add_argument("--no-cli-point", action="store_true", help="skip the 1-GPU CLI runs (-b 1 and -b 8)")
@@ -330,7 +339,7 @@ def cli_serve(args, world, B, passes, warmup):
         with open(fx_path) as f:
             fx = json.load(f)
         if len(fx["outputs"]) >= n:
-            check = compare_request_file(got, fx, n)
+            check = compare_request_file(got, fx, n, REQUEST_TIE_7B, REQUEST_TIE_7B)
             check["tokens_equal_fixture"] = tokens == (sum(fx["achieved_tokens"][:n]) * len(timed_p))
     # per pass, per GPU (worker): tokens, requests, seconds from the pass start to its last step
     per_gpu = {}
@@ -509,6 +518,8 @@ def main(argv=None):
             dec.set(tl.OPT_ATTN_SPLITS, args.splits)
         if args.no_persistent:
             dec.set(tl.OPT_PERSISTENT, 0)
+        if args.no_fuse:
+            dec.set(tl.OPT_FUSE_ATTN_WO, 0)
         return state, dec
 
     def launch_bytes(B, kclass, pos):
@@ -561,15 +572,18 @@ def main(argv=None):
             run(prof_ml)
             dec.set(tl.OPT_PERSISTENT, 1)
         # HBM traffic of the same kernel from the committed rocprofv3 PMC passes (FETCH_SIZE and
-        # WRITE_SIZE in separate runs, gfx950 FETCH_SIZE x2 correction): profiles/*pmc_traffic*.json
+        # WRITE_SIZE in separate runs, gfx950 FETCH_SIZE x2 correction): the newest
+        # profiles/r*_pmc_traffic*.json of this model, dtype and batch
+        import glob
         pmc = {}
-        for fn in (f"r04_pmc_traffic_{args.dtype}_b{B}.json", f"r03_pmc_traffic_{args.dtype}_b{B}.json",
-                   "r02_pmc_traffic_int8.json" if q8 else
-                   "r02_pmc_traffic.json"):
+        for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic*.json")), reverse=True):
+            fn = os.path.basename(path)
+            if ("int8" in fn) != q8:
+                continue
             try:
-                with open(os.path.join(REPO, "profiles", fn)) as f:
+                with open(path) as f:
                     j = json.load(f)
-                if j.get("model", mname) == mname and j.get("batch", 1) == B:
+                if j.get("model", "llama2-7B") == mname and j.get("batch", 1) == B:
                     pmc = {"file": fn, "kernels": j["kernels"]}
                     break
             except (OSError, ValueError, KeyError):
@@ -577,7 +591,7 @@ def main(argv=None):
 
         def traffic_of(prefix):
             hits = [v["traffic_bytes"] for k, v in pmc.get("kernels", {}).items() if k.startswith(prefix)]
-            return round(hits[0]) if hits and mname == "llama2-7B" else None
+            return round(hits[0]) if hits else None
         stp, ffn = prof.get("step"), prof.get("ffn_up")
         roof = None
         if stp:
@@ -646,7 +660,7 @@ def main(argv=None):
                     fx = json.load(f)
                 if len(fx["outputs"]) >= n:
                     got = f"{n}\n".encode() + b"".join(o + b"\n" for o in outs)
-                    check = compare_request_file(got, fx, n)
+                    check = compare_request_file(got, fx, n, REQUEST_TIE_7B, REQUEST_TIE_7B)
             tok_s = gen[0] * passes / el
             dec_tokens = gen[0] - prompt_pos
             per_rank_roof = HBM_PEAK_GBS * 1e9 / token_bytes(B, (T - 1) / 2.0) * B

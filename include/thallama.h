@@ -35,17 +35,24 @@ enum {
   THALLAMA_OPT_PERSISTENT = 5,   /* 0/1: whole step as ONE persistent launch (fp32 batch 1..8,
                                     int8 batch 1; head size 64/128).  Default 1 where supported,
                                     except fp32 batch 5..8 (default 0: slower than multi-launch
-                                    there; env THALLAMA_BATCH_PERSIST=N moves the bound, 0 never
-                                    prepares it).  Profiled as the single class THALLAMA_K_STEP. */
+                                    there).  Profiled as the single class THALLAMA_K_STEP. */
   THALLAMA_OPT_PERSIST_FAULT = 6,  /* test hook: the next persistent launch runs without its
                                     block 0 (as if the grid were not co-resident): its waits
                                     give up, the call disables the path and re-runs on the
-                                    multi-launch step. */
+                                    multi-launch step; with THALLAMA_OPT_FUSE_ATTN_WO on, the
+                                    next fused attention + Wo launch the same way. */
+  THALLAMA_OPT_FUSE_ATTN_WO = 7,   /* 0/1: the multi-launch fp32 step at batch 5..8 runs each
+                                    layer's attention and Wo (+ residual) as ONE launch
+                                    (attn_wo.hip; default 1 where the shape allows).  Profiled
+                                    as THALLAMA_K_ATTN (THALLAMA_K_WO then stays empty). */
 };
 
 /* 1 if the decoder runs its steps as one persistent launch (THALLAMA_OPT_PERSISTENT
  * requested and the shape supported), else 0. */
 int thallama_decoder_persistent(thallama_decoder* d);
+/* 1 if the decoder's multi-launch steps fuse attention and Wo (THALLAMA_OPT_FUSE_ATTN_WO requested,
+ * the shape supported, and no launch of it gave up), else 0. */
+int thallama_decoder_fused_attn_wo(thallama_decoder* d);
 /* 1 if the persistent step is dispatched as a cooperative launch (the runtime checks the grid's
  * co-residency; replays of a captured step keep cooperative dispatch on ROCm 7.2 by observation,
  * and every wait is bounded either way), 0 for a plain launch (THALLAMA_PERSIST_COOP=0 or no
@@ -138,7 +145,7 @@ int thallama_decoder_stage(thallama_decoder* d, const int* token_h, const int* p
  * one decoder per (device, stream, batch, config, dtype), made for the caller's weight and state
  * buffers; a call with other buffers replaces it, and at most cap stay cached (least recently used
  * dropped; the cap starts at 8 and grows by one, up to 256, whenever a recently dropped key comes
- * back, so it follows the callers' working set).  Concurrent callers are safe: a dropped decoder is
+ * back, so it follows the callers' working set; clearing the cache resets the cap).  Concurrent callers are safe: a dropped decoder is
  * freed when the last call using it returns.  The cached count, the cap, the live count (cached +
  * dropped but still running), and a way to drop them all (e.g. before the caller frees its
  * buffers). */

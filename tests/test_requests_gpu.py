@@ -7,9 +7,11 @@ the oracle's lockstep forward (bit-identical to the reference's src/seq.cpp; its
 against the reference's own 256 tokens).  Distinct prompts at distinct positions in one batch at 7B.
 
 A request's output must equal the fixture's byte for byte, except a request that reaches a near-tie
-of the CPU reference (top-2 margin < 1e-4) and takes the other branch there (bench.compare_request_file,
-the rule of tests/test_cli_gpu.py::test_gen_in_128_greedy_fixture); which requests did is printed and
-written under gpurun_out/.
+of the CPU reference and takes the other branch there (bench.compare_request_file, the rule of
+tests/test_cli_gpu.py::test_gen_in_128_greedy_fixture): at 7B a top-2 margin under 2e-4
+(bench.REQUEST_TIE_7B: the GPU's teacher-forced drift from src/seq.cpp peaks at 1.75e-4 over 2048
+steps, the reference's own GPU path's at 5.35e-4), at most as many requests as have such a tie (9 of
+the 64).  Which requests did is printed and written under gpurun_out/.
 """
 import json
 import os
@@ -54,7 +56,7 @@ def run_cli(tmp_path, n, batch, env=None):
 
 
 def check(fx, got, stdout, n, tag):
-    res = bench.compare_request_file(got, fx, n)
+    res = bench.compare_request_file(got, fx, n, bench.REQUEST_TIE_7B, bench.REQUEST_TIE_7B)
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     with open(os.path.join(REPO, "gpurun_out", f"requests_7b_{tag}.json"), "w") as f:
         json.dump(res, f)
