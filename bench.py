@@ -163,8 +163,6 @@ def parse_args(argv):
     ap.add_argument("--splits", type=int, default=0)
     ap.add_argument("--no-persistent", action="store_true",
                     help="multi-launch step instead of the one-launch persistent step")
-    ap.add_argument("--no-fuse", action="store_true",
-                    help="batch 5..8: attention and Wo as two launches instead of one (attn_wo.hip)")
     ap.add_argument("--no-long", action="store_true", help="skip the positions 1792..2047 line")
     ap.add_argument("--no-requests-point", action="store_true", help="skip the 1-GPU request-workload point")
     ap.add_argument("--no-cli-point", action="store_true", help="skip the 1-GPU CLI runs (-b 1 and -b 8)")
@@ -518,8 +516,6 @@ def main(argv=None):
             dec.set(tl.OPT_ATTN_SPLITS, args.splits)
         if args.no_persistent:
             dec.set(tl.OPT_PERSISTENT, 0)
-        if args.no_fuse:
-            dec.set(tl.OPT_FUSE_ATTN_WO, 0)
         return state, dec
 
     def launch_bytes(B, kclass, pos):

@@ -155,10 +155,6 @@ struct AttnWaveParams {
   // [b][dim], group scales [b][dim/64]) so the Wo launch that follows needs no quantise pass
   signed char* xq8;
   float* xq8s;
-  // fp32 multi-launch step with the Wo GEMV in the same launch (attn_wo.hpp): the output row is
-  // stored sc1 and, once drained, counted in done[h] (one add per finished (b, h)); the Wo waves
-  // of other workgroups poll it (MI355X_MICROARCH.md § visibility, Valid forms table row 1)
-  unsigned* done;
 };
 
 TL_DEVICE void st_sc1(float* p, float v) { st1_sc1(p, v); }
@@ -209,17 +205,6 @@ TL_DEVICE void store_head(const AttnWaveParams& w, int b, int h, const float* v,
   constexpr int VPL = HS / 64;
   const AttnParams& p = w.a;
   float* out = p.out + (long long)b * p.dim + h * HS + lane * VPL;
-  if (w.done) {  // handed to the Wo waves of this launch: sc1 stores, drained, then counted
-    if constexpr (VPL == 2) {
-      st2_sc1(out, v[0], v[1]);
-    } else {
-#pragma unroll
-      for (int c = 0; c < VPL; ++c) st1_sc1(out + c, v[c]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_fetch_add(w.done + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
 #pragma unroll
   for (int c = 0; c < VPL; ++c) out[c] = v[c];
   if (!w.xq8) return;

@@ -38,7 +38,6 @@
 #include "persist.hpp"
 #include "prefill.hpp"
 #include "api_lock.hpp"
-#include "attn_wo.hpp"
 
 using tl::f4;
 
@@ -145,6 +144,9 @@ struct thallama_decoder {
   int* pos_h = nullptr;
   int* nxt_h = nullptr;  // pinned: argmax ids of a greedy step
   unsigned* perr_h = nullptr;  // pinned: the persistent step's error word, read back on d->stream
+  float* lg_pin = nullptr;     // pinned staging of a step's logits for pageable caller buffers (logits_dst)
+  const float* lg_last = nullptr;
+  bool lg_last_pinned = false;
   hipEvent_t ev_stage = nullptr;  // pipeline stage done (thallama_decoder_stage)
   // layer streaming (thaDNN_s_forward_70B): the H2D copy stream and, per staging slot, layer
   // copied / layer consumed events
@@ -184,12 +186,6 @@ struct thallama_decoder {
   const signed char* pq8w[7] = {};       // int8: layer-0 int8 block of wq wk wv wo w1 w2 w3
   long long pq8ls[7] = {};                // and the byte stride between layers
   bool pok = false;             // shape supported
-  // fused attention + Wo launch of the batched multi-launch step (attn_wo.hip)
-  unsigned* awo_d = nullptr;    // [H] done counters | workgroup ticket | error word
-  unsigned* awo_err_h = nullptr;  // pinned: the error word, read back with a call's other copies
-  bool awo = true;              // requested (THALLAMA_OPT_FUSE_ATTN_WO)
-  bool awo_ok = false;          // shape supported and no launch gave up
-  bool awo_fault = false;       // test hook (THALLAMA_OPT_PERSIST_FAULT): the next fused launch's waits give up
   unsigned long long* ptrace = nullptr;  // optional timeline of the persistent step
   size_t ptrace_n = 0;
   // batched prompt processing (prefill.hip) for kPrefillChunk tokens, allocated at creation
@@ -411,13 +407,6 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
     TL_TRY(hipMalloc(&d->pgran, sizeof(unsigned long long) * ng));
     TL_TRY(hipMemset(d->pgran, 0, sizeof(unsigned long long) * ng));
   }
-  if (tl::attn_wo_ok(batch, d->dim, d->H, d->hs, d->ncu)) {  // fused attention + Wo (attn_wo.hip)
-    TL_TRY(hipMalloc(&d->awo_d, sizeof(unsigned) * (d->H + 2)));
-    TL_TRY(hipMemset(d->awo_d, 0, sizeof(unsigned) * (d->H + 2)));
-    TL_TRY(hipHostMalloc(&d->awo_err_h, sizeof(unsigned), hipHostMallocDefault));
-    *d->awo_err_h = 0;
-    d->awo_ok = true;
-  }
   *out = d;
   return 0;
 }
@@ -441,6 +430,7 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   (void)hipHostFree(d->pos_h);
   (void)hipHostFree(d->nxt_h);
   (void)hipHostFree(d->perr_h);
+  if (d->lg_pin) (void)hipHostFree(d->lg_pin);
   (void)hipHostFree(d->pf_tok_h);
   (void)hipFree(d->rope_d);
   (void)hipFree(d->xn_d);
@@ -456,8 +446,6 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   (void)hipFree(d->pbmax);
   (void)hipFree(d->pgran);
   (void)hipFree(d->ptrace);
-  (void)hipFree(d->awo_d);
-  (void)hipHostFree(d->awo_err_h);
   for (void* b : {(void*)d->pf_att, (void*)d->pf_x, (void*)d->pf_xn, (void*)d->pf_q, (void*)d->pf_xb, (void*)d->pf_hb,
                   (void*)d->pf_part, (void*)d->pf_cnt, (void*)d->pf_tok, (void*)d->pf_pos})
     (void)hipFree(b);
@@ -475,10 +463,8 @@ extern "C" int thallama_decoder_set(thallama_decoder* d, int key, int value) {
     case THALLAMA_OPT_PERSISTENT: d->persist = value != 0; break;
     case THALLAMA_OPT_PERSIST_FAULT:
       d->pfault = value != 0;
-      d->awo_fault = value != 0;
       drop_graphs(d);
       break;
-    case THALLAMA_OPT_FUSE_ATTN_WO: d->awo = value != 0; break;
     default: return (int)hipErrorInvalidValue;
   }
   drop_graphs(d);  // options are baked into a captured graph: recapture on next use
@@ -588,11 +574,6 @@ static LayerW layer_of(const TransformerWeights& w, int l, long long dim, long l
 }
 
 static bool use_persist(const thallama_decoder* d) { return d->persist && d->pok; }
-// The fused attention + Wo launch on the multi-launch fp32 step (attn_wo.hip).
-static bool use_awo(const thallama_decoder* d) { return d->awo && d->awo_ok && !d->q8 && !use_persist(d); }
-// Which optional launch forms a call may take: a give-up turns one off (check_persist), and the
-// public entry points re-run the call when that set changed.
-static unsigned path_bits(const thallama_decoder* d) { return (use_persist(d) ? 1u : 0u) | (use_awo(d) ? 2u : 0u); }
 
 static int enqueue_step_io(thallama_decoder* d, const StepIO& io) {
   const int dim = d->dim, hid = d->hidden, kvd = d->kv_dim, S = d->S;
@@ -640,34 +621,8 @@ static int enqueue_step_io(thallama_decoder* d, const StepIO& io) {
       TL_TRY(gemv(d, tl::GM_QKV, p, Q8L(wq), Q8L(wk), Q8L(wv)));
       prof_end(d, THALLAMA_K_QKV, ev);
     }
-    // 2 + 3 as one launch: attention, then Wo + residual as its heads complete (attn_wo.hip)
-    const bool fuse = use_awo(d) && io.nb == d->B && io.x == d->s.x && !io.layer_w && !d->q8x;
-    if (fuse) {
-      tl::AttnWoParams P = {};
-      tl::AttnParams& a = P.aw.a;
-      a.q = io.q; a.kc = io.kc; a.vc = io.vc; a.kv_b_stride = kv_b_stride; a.kv_l_off = ll * S * kvd;
-      a.pos = io.pos; a.out = io.xb; a.part = d->part_d;
-      a.dim = dim; a.kv_dim = kvd; a.head_size = d->hs; a.n_heads = d->H; a.kv_mul = d->kv_mul;
-      a.seq_len = S; a.nsplit = d->nsplit; a.min_chunk = 32;
-      P.aw.cnt = d->cnt_d;
-      P.aw.B = io.nb;
-      const int max_chunks = (S + kAttnChunk - 1) / kAttnChunk;
-      P.aw.NS = d->nsplit < max_chunks ? d->nsplit : max_chunks;
-      P.aw.done = d->awo_d;
-      tl::GemvParams& p = P.g;
-      p.W0 = lw.wo; p.K = dim; p.n_items = dim; p.nb = io.nb;
-      p.x = io.xb; p.x_stride = dim; p.y = io.x; p.y_stride = dim;
-      ssq_to_next_norm(d, p);
-      P.done = d->awo_d; P.blocks = d->awo_d + d->H; P.err = d->awo_d + d->H + 1;
-      P.units = io.nb * d->H * P.aw.NS;
-      P.fault = d->awo_fault ? 1 : 0;
-      d->awo_fault = false;  // one-shot, like pfault
-      int ev = prof_begin(d);
-      TL_TRY(tl::launch_attn_wo(P, d->stream));
-      prof_end(d, THALLAMA_K_ATTN, ev);
-    }
     // 2. attention
-    if (!fuse) {
+    {
       tl::AttnParams a = {};
       a.q = io.q;
       a.kc = io.kc;
@@ -734,7 +689,7 @@ static int enqueue_step_io(thallama_decoder* d, const StepIO& io) {
       prof_end(d, THALLAMA_K_ATTN, ev);
     }
     // 3. Wo + residual
-    if (!fuse) {
+    {
       tl::GemvParams p = {};
       p.W0 = lw.wo;
       p.K = dim;
@@ -885,10 +840,6 @@ static int enqueue_err_read(thallama_decoder* d) {
     TL_TRY(hipMemcpyAsync(d->perr_h, d->psync + d->psync_zero, sizeof(unsigned), hipMemcpyDeviceToHost, d->stream));
     d->err_pending = true;
   }
-  if (use_awo(d)) {
-    TL_TRY(hipMemcpyAsync(d->awo_err_h, d->awo_d + d->H + 1, sizeof(unsigned), hipMemcpyDeviceToHost, d->stream));
-    d->err_pending = true;
-  }
   return 0;
 }
 
@@ -896,19 +847,6 @@ static int enqueue_err_read(thallama_decoder* d) {
 static int check_persist(thallama_decoder* d) {
   if (!d->err_pending) return 0;
   d->err_pending = false;
-  if (d->awo_err_h && *d->awo_err_h) {  // a fused attention + Wo launch gave up: its layers are garbage
-    *d->awo_err_h = 0;
-    TL_TRY(hipMemsetAsync(d->awo_d, 0, sizeof(unsigned) * (d->H + 2), d->stream));
-    TL_TRY(hipMemsetAsync(d->cnt_d, 0, sizeof(unsigned) * (size_t)d->B * d->H, d->stream));
-    TL_TRY(hipStreamSynchronize(d->stream));
-    d->awo_ok = false;
-    {
-      ApiLock lock(api_mu());
-      drop_graphs(d);
-    }
-    g_last_error = "fused attention + Wo: a wait timed out (grid not co-resident); path disabled";
-    return kPersistFellBack;
-  }
   if (!*d->perr_h) return 0;
   *d->perr_h = 0;
   TL_TRY(hipMemsetAsync(d->psync, 0, sizeof(unsigned) * (d->psync_zero + 32), d->stream));
@@ -925,7 +863,6 @@ static int check_persist(thallama_decoder* d) {
 }
 
 extern "C" int thallama_decoder_persistent(thallama_decoder* d) { return d && use_persist(d) ? 1 : 0; }
-extern "C" int thallama_decoder_fused_attn_wo(thallama_decoder* d) { return d && use_awo(d) ? 1 : 0; }
 extern "C" int thallama_persistent_cooperative(void) { return tl::persistent_cooperative() ? 1 : 0; }
 
 // Diagnostics: copy the persistent step's hand-off granules {value, tag} (x | xb | hb | q k v |
@@ -1004,10 +941,32 @@ static int upload_tok_pos(thallama_decoder* d, const int* token_h, const int* po
 
 static int decoder_forward_once(thallama_decoder* d, const int* token_h, const int* pos_h, float* logits_h);
 
+// Where a step's B x V logits are copied to: the caller's buffer when it is pinned (the reference
+// passes hipHostMalloc memory, src/llama.cpp:935), else the decoder's pinned staging, copied on
+// after the synchronisation — a D2H copy into pageable memory is staged by the runtime at a fraction
+// of the link rate (1 MB per step at batch 8).  The last buffer's answer is remembered.
+static float* logits_dst(thallama_decoder* d, float* logits_h) {
+  if (logits_h != d->lg_last) {
+    hipPointerAttribute_t a = {};
+    d->lg_last = logits_h;
+    d->lg_last_pinned = hipPointerGetAttributes(&a, logits_h) == hipSuccess && a.type == hipMemoryTypeHost;
+    (void)hipGetLastError();  // (a pageable pointer reports an error: not sticky, cleared here)
+  }
+  if (d->lg_last_pinned) return logits_h;
+  if (!d->lg_pin) {
+    ApiLock lock(api_mu());
+    if (hipHostMalloc(&d->lg_pin, sizeof(float) * (size_t)d->B * d->V, hipHostMallocDefault) != hipSuccess) {
+      d->lg_pin = nullptr;
+      return logits_h;
+    }
+  }
+  return d->lg_pin;
+}
+
 extern "C" int thallama_decoder_forward(thallama_decoder* d, const int* token_h, const int* pos_h, float* logits_h) {
-  const unsigned paths = d ? path_bits(d) : 0u;
+  const bool persistent = d && use_persist(d);
   int r = decoder_forward_once(d, token_h, pos_h, logits_h);
-  if (r == kPersistFellBack && paths != path_bits(d)) r = decoder_forward_once(d, token_h, pos_h, logits_h);
+  if (r == kPersistFellBack && persistent && !use_persist(d)) r = decoder_forward_once(d, token_h, pos_h, logits_h);
   return r;
 }
 
@@ -1033,11 +992,14 @@ static int decoder_forward_once(thallama_decoder* d, const int* token_h, const i
     r = use_persist(d) ? enqueue_persistent(d, false, long_ctx(d, pos_h[0])) : enqueue_step(d);
     if (r) return r;
   }
-  if (logits_h)
-    TL_TRY(hipMemcpyAsync(logits_h, d->s.logits, sizeof(float) * (size_t)d->B * d->V, hipMemcpyDeviceToHost,
-                          d->stream));
+  float* staged = nullptr;
+  if (logits_h) {
+    staged = logits_dst(d, logits_h);
+    TL_TRY(hipMemcpyAsync(staged, d->s.logits, sizeof(float) * (size_t)d->B * d->V, hipMemcpyDeviceToHost, d->stream));
+  }
   if ((r = enqueue_err_read(d)) != 0) return r;
   TL_TRY(hipStreamSynchronize(d->stream));
+  if (staged && staged != logits_h) memcpy(logits_h, staged, sizeof(float) * (size_t)d->B * d->V);
   prof_collect(d);
   return check_persist(d);
 }
@@ -1090,9 +1052,9 @@ static int decoder_step_argmax_once(thallama_decoder* d, const int* token_h, con
 }
 
 extern "C" int thallama_decoder_step_argmax(thallama_decoder* d, const int* token_h, const int* pos_h, int* next_h) {
-  const unsigned paths = d ? path_bits(d) : 0u;
+  const bool persistent = d && use_persist(d);
   int r = decoder_step_argmax_once(d, token_h, pos_h, next_h);
-  if (r == kPersistFellBack && paths != path_bits(d)) r = decoder_step_argmax_once(d, token_h, pos_h, next_h);
+  if (r == kPersistFellBack && persistent && !use_persist(d)) r = decoder_step_argmax_once(d, token_h, pos_h, next_h);
   return r;
 }
 
@@ -1106,9 +1068,9 @@ extern "C" int thallama_decoder_argmax_cb(void* ctx, int worker, int batch, cons
 
 extern "C" int thallama_decoder_greedy(thallama_decoder* d, const int* token0_h, const int* pos0_h, int n_steps,
                                        int* tokens_out_h, int sync) {
-  const unsigned paths = d ? path_bits(d) : 0u;
+  const bool persistent = d && use_persist(d);
   int r = decoder_greedy_once(d, token0_h, pos0_h, n_steps, tokens_out_h, sync);
-  if (r == kPersistFellBack && paths != path_bits(d))
+  if (r == kPersistFellBack && persistent && !use_persist(d))
     r = decoder_greedy_once(d, token0_h, pos0_h, n_steps, tokens_out_h, sync);
   return r;
 }
@@ -1154,7 +1116,7 @@ static int decoder_greedy_once(thallama_decoder* d, const int* token0_h, const i
   } else if (sync) {
     TL_TRY(hipStreamSynchronize(d->stream));
   } else {
-    d->pasync = d->pasync || (n_steps > 0 && path_bits(d) != 0);
+    d->pasync = d->pasync || (n_steps > 0 && use_persist(d));
     prof_collect(d);
     return 0;
   }

@@ -39,20 +39,12 @@ enum {
   THALLAMA_OPT_PERSIST_FAULT = 6,  /* test hook: the next persistent launch runs without its
                                     block 0 (as if the grid were not co-resident): its waits
                                     give up, the call disables the path and re-runs on the
-                                    multi-launch step; with THALLAMA_OPT_FUSE_ATTN_WO on, the
-                                    next fused attention + Wo launch the same way. */
-  THALLAMA_OPT_FUSE_ATTN_WO = 7,   /* 0/1: the multi-launch fp32 step at batch 5..8 runs each
-                                    layer's attention and Wo (+ residual) as ONE launch
-                                    (attn_wo.hip; default 1 where the shape allows).  Profiled
-                                    as THALLAMA_K_ATTN (THALLAMA_K_WO then stays empty). */
+                                    multi-launch step. */
 };
 
 /* 1 if the decoder runs its steps as one persistent launch (THALLAMA_OPT_PERSISTENT
  * requested and the shape supported), else 0. */
 int thallama_decoder_persistent(thallama_decoder* d);
-/* 1 if the decoder's multi-launch steps fuse attention and Wo (THALLAMA_OPT_FUSE_ATTN_WO requested,
- * the shape supported, and no launch of it gave up), else 0. */
-int thallama_decoder_fused_attn_wo(thallama_decoder* d);
 /* 1 if the persistent step is dispatched as a cooperative launch (the runtime checks the grid's
  * co-residency; replays of a captured step keep cooperative dispatch on ROCm 7.2 by observation,
  * and every wait is bounded either way), 0 for a plain launch (THALLAMA_PERSIST_COOP=0 or no
