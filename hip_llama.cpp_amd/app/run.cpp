@@ -202,6 +202,7 @@ struct Replica {
   float* emb = nullptr;  // int8: dequantised embedding
   RunState* s = nullptr;
   thallama_decoder* dec = nullptr;
+  float* logits_h = nullptr;  // pinned [batch][V]: the sampling steps' logits (src/llama.cpp:935)
 };
 
 static double now_s() {
@@ -437,6 +438,7 @@ static std::vector<Replica> replicate(ModelFile& m, int n_dev, int n_rep, int ba
       exit(EXIT_FAILURE);
     }
     thallama_decoder_set(r.dec, THALLAMA_OPT_USE_GRAPH, 1);  // each step replayed as one captured graph
+    HIP_OK(hipHostMalloc(&r.logits_h, sizeof(float) * (size_t)batch * m.cfg.vocab_size, hipHostMallocDefault));
   }
   return reps;
 }
@@ -446,6 +448,7 @@ static void release(std::vector<Replica>& reps) {
     HIP_OK(hipSetDevice(r.dev));
     thallama_decoder_destroy(r.dec);
     free_state_device(r.s);
+    if (r.logits_h) HIP_OK(hipHostFree(r.logits_h));
     if (r.emb) {
       thallama_q8_unmap(&r.w8);
       HIP_OK(hipFree(r.emb));
@@ -665,10 +668,12 @@ int main(int argc, char* argv[]) {
       std::vector<long long> w_tok((size_t)n_rep, 0);
       std::vector<double> w_sec((size_t)n_rep, 0.0);
       std::vector<int> w_req((size_t)n_rep, 0);
+      std::vector<float*> w_lg((size_t)n_rep);
+      for (int w = 0; w < n_rep; ++w) w_lg[w] = reps[w].logits_h;
       const int st = thallama_serve_requests_stats(req, tokenizer_path, V, n_rep, batch, replica_step,
                                                    getenv("THALLAMA_HOST_ARGMAX") ? nullptr : replica_argmax,
                                                    replica_prefill, &reps, &num_gen_tokens, w_tok.data(), w_sec.data(),
-                                                   w_req.data());
+                                                   w_req.data(), w_lg.data());
       const long end = time_in_ms();
       if (st != 0) {
         fprintf(stderr, "test mode failed (%d)\n", st);

@@ -318,14 +318,14 @@ extern "C" int thallama_serve_requests_greedy(thallama_requests* r, const char* 
                                               thallama_argmax_step_fn argmax_step, thallama_prefill_fn prefill,
                                               void* ctx, long long* gen_tokens) {
   return thallama_serve_requests_stats(r, tokenizer_path, vocab_size, n_workers, batch, step, argmax_step, prefill, ctx,
-                                       gen_tokens, nullptr, nullptr, nullptr);
+                                       gen_tokens, nullptr, nullptr, nullptr, nullptr);
 }
 
 extern "C" int thallama_serve_requests_stats(thallama_requests* r, const char* tokenizer_path, int vocab_size,
                                              int n_workers, int batch, thallama_step_fn step,
                                              thallama_argmax_step_fn argmax_step, thallama_prefill_fn prefill,
                                              void* ctx, long long* gen_tokens, long long* worker_tokens,
-                                             double* worker_seconds, int* worker_requests) {
+                                             double* worker_seconds, int* worker_requests, float* const* logits_bufs) {
   if (!r || n_workers <= 0 || batch <= 0) return -1;
   // greedy sampling is sample_argmax of the logits: the device step may take it (only B ids return)
   const bool on_device = argmax_step && r->temperature == 0.0f;
@@ -347,7 +347,10 @@ extern "C" int thallama_serve_requests_stats(thallama_requests* r, const char* t
       status = -2;
       return;
     }
-    std::vector<float> logits(on_device ? 0 : (size_t)batch * V);
+    // the step's logits: the caller's buffer for this worker (e.g. pinned host memory the device
+    // copies into at the link rate, as the reference's hipHostMalloc'd logits_host), else our own
+    std::vector<float> own(on_device || (logits_bufs && logits_bufs[w]) ? 0 : (size_t)batch * V);
+    float* const logits = logits_bufs && logits_bufs[w] ? logits_bufs[w] : own.data();
     std::vector<int> next_ids(batch, 0);
     std::vector<int> req(batch, -1), token(batch, 0), pos(batch, 0), steps(batch, 0), n_prompt(batch, 0);
     std::vector<char> done(batch, 0);
@@ -404,7 +407,7 @@ extern "C" int thallama_serve_requests_stats(thallama_requests* r, const char* t
       if (status != 0) break;
       if (idle == batch) break;
       const int st = on_device ? argmax_step(ctx, w, batch, token.data(), pos.data(), next_ids.data())
-                               : step(ctx, w, batch, token.data(), pos.data(), logits.data());
+                               : step(ctx, w, batch, token.data(), pos.data(), logits);
       if (st != 0) {
         status = st;
         break;
@@ -414,7 +417,7 @@ extern "C" int thallama_serve_requests_stats(thallama_requests* r, const char* t
         int next;
         if (pos[b] < n_prompt[b] - 1) next = prompt[b][pos[b] + 1];  // still in the prompt
         else if (on_device) next = next_ids[b];
-        else next = thallama_sample(samplers[req[b]], logits.data() + (size_t)b * V);
+        else next = thallama_sample(samplers[req[b]], logits + (size_t)b * V);
         pos[b] += 1;
         if (next == 1 || next == 2) {  // BOS / EOS end the sequence
           done[b] = 1;

@@ -95,11 +95,14 @@ int thallama_serve_requests_greedy(thallama_requests* r, const char* tokenizer_p
 /* thallama_serve_requests_greedy with per-worker accounting (each array n_workers long, any may be
  * NULL): worker w's share of *gen_tokens, the requests it finished, and the seconds from the
  * common start to its last step — one worker per GPU, so these are the per-GPU numbers of a
- * multi-GPU run. */
+ * multi-GPU run.  logits_bufs (NULL, or n_workers pointers, each NULL or batch x vocab floats):
+ * the buffer worker w's step callback writes its logits into — pinned host memory lets the device
+ * copy them at the link rate, like the reference's hipHostMalloc'd logits_host. */
 int thallama_serve_requests_stats(thallama_requests* r, const char* tokenizer_path, int vocab_size, int n_workers,
                                   int batch, thallama_step_fn step, thallama_argmax_step_fn argmax_step,
                                   thallama_prefill_fn prefill, void* ctx, long long* gen_tokens,
-                                  long long* worker_tokens, double* worker_seconds, int* worker_requests);
+                                  long long* worker_tokens, double* worker_seconds, int* worker_requests,
+                                  float* const* logits_bufs);
 
 #ifdef __cplusplus
 }

@@ -161,11 +161,14 @@ def test_reference_cli_timed_beside_ours(gpu, oracle, pkg, tmp_path):
     shutil.copy(os.path.join(REPO, "tests", "golden", "tokenizer.bin"), tmp_path / "tokenizer.bin")
     res = {}
     outs = {}
-    for name, exe in (("reference_cli_on_libthallama", BUILT), ("this_cli", os.path.join(REPO, "build", "apps", "llama"))):
+    ours = os.path.join(REPO, "build", "apps", "llama")
+    for name, exe, env in (("reference_cli_on_libthallama", BUILT, {}), ("this_cli", ours, {}),
+                           ("this_cli_prompts_stepped", ours, {"THALLAMA_NO_PREFILL": "1"})):
         out = tmp_path / f"out_{name}.txt"
         t0 = time.perf_counter()
         r = subprocess.run([exe, path, "-m", "test", "-f", str(inp), "-o", str(out), "-b", "8", "-z",
-                            str(tmp_path / "tokenizer.bin")], cwd=tmp_path, capture_output=True, text=True, timeout=600)
+                            str(tmp_path / "tokenizer.bin")], cwd=tmp_path, capture_output=True, text=True, timeout=600,
+                           env={**os.environ, **env})
         wall = time.perf_counter() - t0
         assert r.returncode == 0, r.stderr[-2000:]
         tot = [ln for ln in r.stdout.splitlines() if ln.startswith("Total achieved token:")]
@@ -173,7 +176,7 @@ def test_reference_cli_timed_beside_ours(gpu, oracle, pkg, tmp_path):
         tokens, secs = int(tot[-1].split()[-1]), float(el[-1].split()[2].rstrip(","))
         res[name] = {"tokens": tokens, "seconds": secs, "tok_s": round(tokens / secs, 1), "wall_s": round(wall, 2)}
         outs[name] = out.read_bytes()
-    res["outputs_equal"] = outs["reference_cli_on_libthallama"] == outs["this_cli"]
+    res["outputs_equal"] = outs["reference_cli_on_libthallama"] == outs["this_cli"] == outs["this_cli_prompts_stepped"]
     res["workload"] = (f"stories110M-shaped fp32 v0 file (classifier x30), first {n} prompts of gen_in_128.txt, -m test "
                        "-b 8 (T=1.0, top-p 0.9, seed 314028 per request), each request to seq_len 1024 or BOS/EOS")
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
