@@ -3,6 +3,8 @@
 
     python tools/rocprof_summary.py stats <results.db> <out.csv>
         kernel, calls, total_us, avg_us, percent  (the top_kernels view of --kernel-trace --stats)
+    python tools/rocprof_summary.py counters <results.db> <out.json> [note]
+        per-kernel launch averages of every counter of one --pmc pass
     python tools/rocprof_summary.py pmc <fetch_results.db> <write_results.db> <out.json> [note] [model] [batch]
         per-kernel launch averages of FETCH_SIZE / WRITE_SIZE (separate --pmc passes) and
         traffic_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (gfx950: FETCH_SIZE counts half of
@@ -52,8 +54,25 @@ def pmc(fetch_db, write_db, out, note="", model=None, batch=None):
         json.dump({**head, "kernels": res}, fo, indent=1)
 
 
+
+
+def counters_json(db, out, note=""):
+    """Per-kernel launch averages of every counter a --pmc pass collected (any names)."""
+    con = sqlite3.connect(db)
+    acc = {}
+    for kname, cname, val in con.execute("select kernel_name, counter_name, value from counters_collection"):
+        s = acc.setdefault(kname, {}).setdefault(cname, [0.0, 0])
+        s[0] += val
+        s[1] += 1
+    res = {k: {c: {"avg": v[0] / v[1], "launches": v[1]} for c, v in cs.items()} for k, cs in acc.items()}
+    with open(out, "w") as fo:
+        json.dump({"_how": note, "kernels": res}, fo, indent=1)
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3])
+    elif sys.argv[1] == "counters":
+        counters_json(sys.argv[2], sys.argv[3], sys.argv[4] if len(sys.argv) > 4 else "")
     else:
         pmc(*sys.argv[2:5], *sys.argv[5:8])
