@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--model", default="7b", choices=sorted(MODELS))
     ap.add_argument("--pos", type=int, default=8, help="position of the traced step")
     ap.add_argument("--json", default="")
+    ap.add_argument("--npz", default="", help="also save the raw stamps [grid][phase][slot] (100-MHz ticks)")
     ap.add_argument("--dtype", default="f32", choices=["f32", "int8"])
     ap.add_argument("--batch", type=int, default=1, help="sequences (2..8: the batched step, persist_b.hip)")
     args = ap.parse_args()
@@ -52,6 +53,8 @@ def main():
     G = t.size // (nph * NSL)
     t = t.reshape(G, nph, NSL)
     raw = t.copy()  # (slot 13 holds a count, not a time)
+    if args.npz:
+        np.savez_compressed(args.npz, stamps=raw)
     t = (t - t[:, 0, 0].min()) * 0.01  # us
     dim, hid, kvd, V = cfg[0], cfg[1], cfg[0] * cfg[4] // cfg[3], cfg[5]
     esz = 4 if args.dtype == "f32" else 1 + 4 / 64  # int8 + one fp32 scale per 64
