@@ -164,6 +164,8 @@ def parse_args(argv):
     ap.add_argument("--no-persistent", action="store_true",
                     help="multi-launch step instead of the one-launch persistent step")
     ap.add_argument("--no-long", action="store_true", help="skip the positions 1792..2047 line")
+    ap.add_argument("--long-kernels", action="store_true",
+                    help="also time each kernel class with HIP events over the long-context tail (eager replay)")
     ap.add_argument("--no-requests-point", action="store_true", help="skip the 1-GPU request-workload point")
     ap.add_argument("--no-cli-point", action="store_true", help="skip the 1-GPU CLI runs (-b 1 and -b 8)")
     ap.add_argument("--host-argmax", action="store_true",
@@ -759,6 +761,22 @@ def main(argv=None):
                         "achieved_GBps": round(tail_bytes * t_tail / lt / 1e9, 1),
                         "frac_of_peak": round(tail_bytes * t_tail / lt / 1e9 / HBM_PEAK_GBS, 4),
                         "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / tail_bytes * B, 1)}
+            if args.long_kernels:
+                # per-kernel-class HIP events over the same tail, replayed eagerly (the K/V rows it
+                # rewrites are the ones already there); GB/s from each class's algorithmic bytes at
+                # the tail's positions (attention: the K/V rows it reads)
+                dec.set(tl.OPT_PROFILE, 1)
+                dec.prof_reset()
+                dec.greedy(last_tok, [S - t_tail] * B, t_tail, want_tokens=False, sync=True)
+                kk = {}
+                for k, name in enumerate(tl.K_NAMES):
+                    ms, n = dec.prof(k)
+                    if n:
+                        us = 1e3 * ms / n
+                        kb = sum(launch_bytes(B, k, [p] * B) for p in range(S - t_tail, S)) / t_tail
+                        kk[name] = {"avg_us": round(us, 2), "launches": n, "GBps": round(kb / (us * 1e-6) / 1e9, 1)}
+                dec.set(tl.OPT_PROFILE, 0)
+                long_ctx["kernels_eager"] = kk
             try:
                 with open(os.path.join(GOLDEN, "reference_2048.json")) as f:
                     g2 = json.load(f)

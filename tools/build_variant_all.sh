@@ -7,7 +7,7 @@ name=$1; shift
 out=/tmp/variants/$name; mkdir -p $out
 for f in csrc/*.hip; do
   b=$(basename $f .hip)
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -Wall -Wno-unused-function \
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -ffp-contract=off -Wall -Wno-unused-function \
     -I../include $* -c $f -o $out/$b.o &
   while [ $(jobs -r | wc -l) -ge 8 ]; do sleep 1; done
 done
