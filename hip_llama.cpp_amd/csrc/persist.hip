@@ -593,9 +593,9 @@ TL_DEVICE void preload_rms(const float* w, int dim, float* rmsw, int lane) {
 }
 
 // (cos, sin) of the RoPE pair at QKV row `row` (< dim + kv_dim) for this step's position.
-TL_DEVICE float2 rope_cs(const PStep& p, int row) {
+TL_DEVICE float2 rope_cs(const PStep& p, int pb, int row) {
   const int i = row < p.dim ? row : row - p.dim;
-  return p.rope[(long long)p.pos[0] * (p.hs >> 1) + ((i % p.hs) >> 1)];
+  return p.rope[(long long)pb * (p.hs >> 1) + ((i % p.hs) >> 1)];
 }
 
 // Control wave: row values from the LDS row-chunk sums, fused epilogue, granule stores.
@@ -606,7 +606,7 @@ TL_DEVICE float2 rope_cs(const PStep& p, int row) {
 // int8: the body with the phase kind read at run time (the per-kind instantiations below cost the
 // int8 step 0.6-0.8%: profiles/r04/epilogue_kind_ab.txt).
 TL_DEVICE void epilogue_rt(const PDesc& d, const PGeo& g, const PStep& p, const float* res, float* xres, int lane,
-                        int l, float2 cs0, const float* pbuf, const uint64_t* etab) {
+                        int l, int pb, float2 cs0, const float* pbuf, const uint64_t* etab) {
   unsigned long long best = 0;
   for (int it = lane; it < g.ni; it += 64) {
     float v[2] = {0.f, 0.f};
@@ -638,10 +638,9 @@ TL_DEVICE void epilogue_rt(const PDesc& d, const PGeo& g, const PStep& p, const 
       st8_sc1(d.gout + item, gran(d.tag_out, silu_mul_tab(v[0], v[1], etab)));
     } else {  // PK_QKV: RoPE (src/seq.cpp:86-101), q / k_new / v_new granules, KV-cache row
       const int row = 2 * item;
-      const int pb = p.pos[0];
       float a0 = v[0], a1 = v[1];
       if (row < p.dim + p.kvd) {
-        const float2 cs = it == lane ? cs0 : rope_cs(p, row);
+        const float2 cs = it == lane ? cs0 : rope_cs(p, pb, row);
         const float r0 = __fsub_rn(__fmul_rn(a0, cs.x), __fmul_rn(a1, cs.y));
         const float r1 = __fadd_rn(__fmul_rn(a0, cs.y), __fmul_rn(a1, cs.x));
         a0 = r0; a1 = r1;
@@ -671,7 +670,7 @@ TL_DEVICE void epilogue_rt(const PDesc& d, const PGeo& g, const PStep& p, const 
 // Wo / W1-W3 / W2; 7B +1.0-1.4%, 110M +1.9%, profiles/r04/epilogue_kind_ab.txt).
 template <int KIND>
 TL_DEVICE void epilogue_k(const PDesc& d, const PGeo& g, const PStep& p, const float* res, float* xres, int lane,
-                          int l, float2 cs0, const uint64_t* etab) {
+                          int l, int pb, float2 cs0, const uint64_t* etab) {
   constexpr int kind = KIND, rpi = KIND == PK_QKV || KIND == PK_UP ? 2 : 1;
   unsigned long long best = 0;
   for (int it = lane; it < g.ni; it += 64) {
@@ -702,10 +701,9 @@ TL_DEVICE void epilogue_k(const PDesc& d, const PGeo& g, const PStep& p, const f
       st8_sc1(d.gout + item, gran(d.tag_out, silu_mul_tab(v[0], v[1], etab)));
     } else {  // PK_QKV: RoPE (src/seq.cpp:86-101), q / k_new / v_new granules, KV-cache row
       const int row = 2 * item;
-      const int pb = p.pos[0];
       float a0 = v[0], a1 = v[1];
       if (row < p.dim + p.kvd) {
-        const float2 cs = it == lane ? cs0 : rope_cs(p, row);
+        const float2 cs = it == lane ? cs0 : rope_cs(p, pb, row);
         const float r0 = __fsub_rn(__fmul_rn(a0, cs.x), __fmul_rn(a1, cs.y));
         const float r1 = __fadd_rn(__fmul_rn(a0, cs.y), __fmul_rn(a1, cs.x));
         a0 = r0; a1 = r1;
@@ -731,17 +729,17 @@ TL_DEVICE void epilogue_k(const PDesc& d, const PGeo& g, const PStep& p, const f
 
 template <bool Q8>
 TL_DEVICE void epilogue(const PDesc& d, const PGeo& g, const PStep& p, const float* res, float* xres, int lane,
-                        int l, float2 cs0, const float* pbuf, const uint64_t* etab) {
+                        int l, int pb, float2 cs0, const float* pbuf, const uint64_t* etab) {
   if constexpr (Q8) {
-    epilogue_rt(d, g, p, res, xres, lane, l, cs0, pbuf, etab);
+    epilogue_rt(d, g, p, res, xres, lane, l, pb, cs0, pbuf, etab);
     return;
   }
   switch (d.kind) {
-    case PK_QKV: epilogue_k<PK_QKV>(d, g, p, res, xres, lane, l, cs0, etab); break;
-    case PK_WO: epilogue_k<PK_WO>(d, g, p, res, xres, lane, l, cs0, etab); break;
-    case PK_UP: epilogue_k<PK_UP>(d, g, p, res, xres, lane, l, cs0, etab); break;
-    case PK_DOWN: epilogue_k<PK_DOWN>(d, g, p, res, xres, lane, l, cs0, etab); break;
-    default: epilogue_k<PK_CLS>(d, g, p, res, xres, lane, l, cs0, etab); break;
+    case PK_QKV: epilogue_k<PK_QKV>(d, g, p, res, xres, lane, l, pb, cs0, etab); break;
+    case PK_WO: epilogue_k<PK_WO>(d, g, p, res, xres, lane, l, pb, cs0, etab); break;
+    case PK_UP: epilogue_k<PK_UP>(d, g, p, res, xres, lane, l, pb, cs0, etab); break;
+    case PK_DOWN: epilogue_k<PK_DOWN>(d, g, p, res, xres, lane, l, pb, cs0, etab); break;
+    default: epilogue_k<PK_CLS>(d, g, p, res, xres, lane, l, pb, cs0, etab); break;
   }
 }
 
@@ -797,6 +795,9 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
     for (int it = lane; it < gx.ni; it += 64) xres[it] = er[it];
     preload_rms(p.L > 0 ? p.rms_att : p.rms_final, p.dim, rmsw, lane);
     if (lane == 0) *ctr = 0u;
+    // the step's position, read once: the QKV epilogues' cache-row address and RoPE rows (a
+    // global read there put a scalar-cache miss behind every layer's granule publish)
+    const int pos_b = p.pos[0];
     __syncthreads();  // first norm weights preloaded
     // the attention units of layer l (fp32 at long contexts: twice the key splits, the helper)
     const bool help = !Q8 && HELP && p.attn_help && p.pos[0] + 1 >= kAttnHelpMinKeys;
@@ -846,13 +847,13 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
       float2 cs0 = make_float2(1.f, 0.f);
       if (kind == PK_QKV) {
         preload_rms(p.rms_ffn + (long long)l * p.dim, p.dim, rmsw, lane);
-        if (lane < g.ni && 2 * (g.i0 + lane) < p.dim + p.kvd) cs0 = rope_cs(p, 2 * (g.i0 + lane));
+        if (lane < g.ni && 2 * (g.i0 + lane) < p.dim + p.kvd) cs0 = rope_cs(p, pos_b, 2 * (g.i0 + lane));
       }
       if (kind == PK_UP) preload_rms(l + 1 < p.L ? p.rms_att + (long long)(l + 1) * p.dim : p.rms_final, p.dim, rmsw, lane);
       __syncthreads();  // every slot reduced into res
       if (lane == 0) *ctr = 0u;  // next GEMV phase's slot counter (used after its staging barrier)
       TRACE(2);
-      epilogue<Q8>(d, g, p, res, xres, lane, l, cs0, scr, etab);
+      epilogue<Q8>(d, g, p, res, xres, lane, l, pos_b, cs0, scr, etab);
       TRACE(3);
     }
   } else {
