@@ -155,6 +155,7 @@ struct AttnWaveParams {
   // [b][dim], group scales [b][dim/64]) so the Wo launch that follows needs no quantise pass
   signed char* xq8;
   float* xq8s;
+  int poll_long;  // persistent step of a large model: granule waits back off (common.hpp gran_backoff)
 };
 
 TL_DEVICE void st_sc1(float* p, float v) { st1_sc1(p, v); }
@@ -311,23 +312,23 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
 #pragma unroll
           for (int c = 0; c < VPL; ++c) vr[c] = ld8_sc1(gq + vo / 8 + c);
         }
-        qv = gran4_ok(qa, qb, w.tag_in) ? gran4_val(qa, qb) : gran_wait4(rg, qo, w.tag_in, w.err);
+        qv = gran4_ok(qa, qb, w.tag_in) ? gran4_val(qa, qb) : gran_wait4(rg, qo, w.tag_in, w.err, w.poll_long != 0);
         qready = true;
         if (w.ts && lane == 0) w.ts[0] = __builtin_amdgcn_s_memrealtime();
         if (t1 == T) {
-          kn = gran4_ok(ka, kb, w.tag_in) ? gran4_val(ka, kb) : gran_wait4(rg, ko, w.tag_in, w.err);
+          kn = gran4_ok(ka, kb, w.tag_in) ? gran4_val(ka, kb) : gran_wait4(rg, ko, w.tag_in, w.err, w.poll_long != 0);
 #pragma unroll
           for (int c = 0; c < VPL; ++c)
             vn[c] = (unsigned)(vr[c] >> 32) == w.tag_in ? __uint_as_float((unsigned)vr[c])
-                                                       : gran_wait(gq + vo / 8 + c, w.tag_in, w.err);
+                                                       : gran_wait(gq + vo / 8 + c, w.tag_in, w.err, w.poll_long != 0);
           kvready = true;
         }
       }
       if (t1 == T) {  // this chunk holds the new row
         if (!kvready) {
-          kn = gran_wait4(rg, ko, w.tag_in, w.err);
+          kn = gran_wait4(rg, ko, w.tag_in, w.err, w.poll_long != 0);
 #pragma unroll
-          for (int c = 0; c < VPL; ++c) vn[c] = gran_wait(gq + vo / 8 + c, w.tag_in, w.err);
+          for (int c = 0; c < VPL; ++c) vn[c] = gran_wait(gq + vo / 8 + c, w.tag_in, w.err, w.poll_long != 0);
         }
         if (w.ts && lane == 0) w.ts[1] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
@@ -547,7 +548,7 @@ TL_DEVICE void attn_unit_split(const AttnWaveParams& w, int h, int c, int NG, fl
     for (int cc = 0; cc < VPL; ++cc)
       dst[r][lane * VPL + cc] = (unsigned)(g[r][cc] >> 32) == w.tag_in
                                     ? __uint_as_float((unsigned)g[r][cc])
-                                    : gran_wait(src[r] + lane * VPL + cc, w.tag_in, w.err);
+                                    : gran_wait(src[r] + lane * VPL + cc, w.tag_in, w.err, w.poll_long != 0);
   if (w.ts && lane == 0) w.ts[0] = __builtin_amdgcn_s_memrealtime();
   wave_lds_fence();
   const f4* q4 = reinterpret_cast<const f4*>(qs);
@@ -587,7 +588,7 @@ TL_DEVICE void attn_unit_split(const AttnWaveParams& w, int h, int c, int NG, fl
   float mx = -__builtin_inff();
   for (int t = lane; t < T; t += 64) {
     const unsigned long long x = ld8_sc1(gs + t);
-    const float sc = (unsigned)(x >> 32) == w.tag_out ? __uint_as_float((unsigned)x) : gran_wait(gs + t, w.tag_out, w.err);
+    const float sc = (unsigned)(x >> 32) == w.tag_out ? __uint_as_float((unsigned)x) : gran_wait(gs + t, w.tag_out, w.err, w.poll_long != 0);
     at[t] = sc;
     mx = fmaxf(mx, sc);
   }
@@ -688,8 +689,25 @@ TL_DEVICE void win_issue(const float* base, int kv_dim, int t0, int n, bool mult
   }
 }
 
+// A single-round unit's cached K/V rows (written by earlier launches) requested into its window
+// ahead of the attention phase, while the QKV phase streams: issued at the phase start they
+// queued behind the CU's own next-phase weight prefetch (~2 us at short contexts).  Returns
+// whether it issued them (then attn_unit_win(..., pre = true) does not).
 template <int HS>
-TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int lane) {
+TL_DEVICE bool attn_win_preissue(const AttnWaveParams& w, int unit, float* win, int lane) {
+  const WinUnit u = win_unit(w, unit);
+  if (!u.live || u.k0 >= u.ke || u.ke - u.k0 > 64) return false;
+  const AttnParams& p = w.a;
+  const int kvh = u.h / p.kv_mul;
+  const float* kbase = p.kc + (long long)u.b * p.kv_b_stride + p.kv_l_off + (long long)kvh * HS;
+  const float* vbase = p.vc + (long long)u.b * p.kv_b_stride + p.kv_l_off + (long long)kvh * HS;
+  win_issue<HS>(kbase, p.kv_dim, u.k0, u.ke - u.k0, false, win, lane);
+  win_issue<HS>(vbase, p.kv_dim, u.k0, u.ke - u.k0, false, win + 64 * HS, lane);
+  return true;
+}
+
+template <int HS>
+TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int lane, bool pre = false) {
   constexpr int VPL = HS / 64;
   constexpr int PC = HS / 4;     // 16-B pieces per row
   constexpr int RPI = 256 / HS;  // V rows per 1-KiB DMA instruction
@@ -722,7 +740,7 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
     if constexpr (PC == 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   };
-  if (k0 < ke) {  // the first round is in flight before q has arrived
+  if (k0 < ke && !pre) {  // the first round is in flight before q has arrived
     issue_k(k0, min(64, ke - k0));
     issue_v(k0, min(64, ke - k0));
   }
@@ -746,12 +764,12 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
 #pragma unroll
     for (int c = 0; c < VPL; ++c) {
       qs[lane * VPL + c] = (unsigned)(g[0][c] >> 32) == w.tag_in ? __uint_as_float((unsigned)g[0][c])
-                                                                  : gran_wait(srcq + lane * VPL + c, w.tag_in, w.err);
+                                                                  : gran_wait(srcq + lane * VPL + c, w.tag_in, w.err, w.poll_long != 0);
       if (last) {
         kn[lane * VPL + c] = (unsigned)(g[1][c] >> 32) == w.tag_in ? __uint_as_float((unsigned)g[1][c])
-                                                                    : gran_wait(srck + lane * VPL + c, w.tag_in, w.err);
+                                                                    : gran_wait(srck + lane * VPL + c, w.tag_in, w.err, w.poll_long != 0);
         vn[c] = (unsigned)(g[2][c] >> 32) == w.tag_in ? __uint_as_float((unsigned)g[2][c])
-                                                       : gran_wait(srcv + lane * VPL + c, w.tag_in, w.err);
+                                                       : gran_wait(srcv + lane * VPL + c, w.tag_in, w.err, w.poll_long != 0);
       }
     }
   }

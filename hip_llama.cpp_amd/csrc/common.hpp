@@ -227,8 +227,18 @@ TL_DEVICE unsigned long long gran(unsigned tag, float v) {
   return ((unsigned long long)tag << 32) | __float_as_uint(v);
 }
 constexpr unsigned kGranSpinLimit = 1u << 18;
+// Pause between re-polls of a late granule: 64 cycles; with lng (the persistent step's input
+// sweeps of a large model, whose phases last 6-60 us) 512 after the second re-poll and 2048 after
+// the sixth, since hundreds of waves re-polling every ~1 us load the fabric the weight stream uses
+// (7B fp32 +1.2%, int8 +1.3%; a model whose hand-offs are 1-3 us loses from the added latency:
+// 110M -3.5% with every wait long, profiles/r05/gran_poll_ab.txt).
+TL_DEVICE void gran_backoff(unsigned spins, bool lng) {
+  if (lng && spins >= 6) __builtin_amdgcn_s_sleep(32);
+  else if (lng && spins >= 2) __builtin_amdgcn_s_sleep(8);
+  else __builtin_amdgcn_s_sleep(1);
+}
 // Bounded wait for one granule; a give-up (or an error already flagged) sets/keeps *err = 2.
-TL_DEVICE float gran_wait(const unsigned long long* g, unsigned tag, unsigned* err) {
+TL_DEVICE float gran_wait(const unsigned long long* g, unsigned tag, unsigned* err, bool lng = false) {
   for (unsigned spins = 0;; ++spins) {
     const unsigned long long x = ld8_sc1(g);
     if ((unsigned)(x >> 32) == tag) return __uint_as_float((unsigned)x);
@@ -237,7 +247,7 @@ TL_DEVICE float gran_wait(const unsigned long long* g, unsigned tag, unsigned* e
       __hip_atomic_store(as_g32(err), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return __uint_as_float((unsigned)x);
     }
-    __builtin_amdgcn_s_sleep(1);
+    gran_backoff(spins, lng);
   }
 }
 // Four consecutive granules (a float4) at byte offset off (32-B aligned) of resource r.
@@ -250,7 +260,7 @@ TL_DEVICE f4 gran4_val(v4u a, v4u b) {
 TL_DEVICE v4u ld16_sc1(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kSC1);
 }
-TL_DEVICE f4 gran_wait4(__amdgpu_buffer_rsrc_t r, unsigned off, unsigned tag, unsigned* err) {
+TL_DEVICE f4 gran_wait4(__amdgpu_buffer_rsrc_t r, unsigned off, unsigned tag, unsigned* err, bool lng = false) {
   for (unsigned spins = 0;; ++spins) {
     const v4u a = ld16_sc1(r, off), b = ld16_sc1(r, off + 16);
     if (gran4_ok(a, b, tag)) return gran4_val(a, b);
@@ -259,7 +269,7 @@ TL_DEVICE f4 gran_wait4(__amdgpu_buffer_rsrc_t r, unsigned off, unsigned tag, un
       __hip_atomic_store(as_g32(err), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return gran4_val(a, b);
     }
-    __builtin_amdgcn_s_sleep(1);
+    gran_backoff(spins, lng);
   }
 }
 // Two granules {a, b} with one 16-byte sc1 store (off 16-B aligned).

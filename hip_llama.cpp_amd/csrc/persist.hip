@@ -416,7 +416,7 @@ TL_DEVICE void put_squares(float* sqa, int ch, int j, f4 v) {
 // vmcnt waits exact (int8, where mid issues slots); otherwise only threads with input load.
 template <int NB, bool UNC, class F>
 TL_DEVICE void gather(__amdgpu_buffer_rsrc_t r, unsigned tag, int n4, int pad4, int t, int T, f4* xs, float& sq,
-                      unsigned* err, float* sqa, int sqch, F&& mid) {
+                      unsigned* err, bool lng, float* sqa, int sqch, F&& mid) {
   for (int k0 = 0; k0 * T < pad4; k0 += NB) {
     v4u a[NB], b[NB];
 #pragma unroll
@@ -434,7 +434,7 @@ TL_DEVICE void gather(__amdgpu_buffer_rsrc_t r, unsigned tag, int n4, int pad4, 
       if (j < pad4) {
         f4 v = f4{0.f, 0.f, 0.f, 0.f};
         if (j < n4)
-          v = gran4_ok(a[k], b[k], tag) ? gran4_val(a[k], b[k]) : gran_wait4(r, (unsigned)j * 32u, tag, err);
+          v = gran4_ok(a[k], b[k], tag) ? gran4_val(a[k], b[k]) : gran_wait4(r, (unsigned)j * 32u, tag, err, lng);
         sq = fmaf(v.x, v.x, sq); sq = fmaf(v.y, v.y, sq); sq = fmaf(v.z, v.z, sq); sq = fmaf(v.w, v.w, sq);
         xs[j] = v;
         if (sqa && j < n4) put_squares(sqa, sqch, j, v);
@@ -450,7 +450,7 @@ TL_DEVICE void gather(__amdgpu_buffer_rsrc_t r, unsigned tag, int n4, int pad4, 
 // up to nch whole chunks get scale 0 (the products there are 0 * 0).
 template <int NB, class F>
 TL_DEVICE void gather_q8(__amdgpu_buffer_rsrc_t r, unsigned tag, int n4, int nch, signed char* xq, float* xsc,
-                         unsigned* err, F&& mid) {
+                         unsigned* err, bool lng, F&& mid) {
   const int t = threadIdx.x, lane = t & 63;
   for (int k0 = 0; k0 * PT < n4; k0 += NB) {
     v4u a[NB], b[NB];
@@ -466,7 +466,7 @@ TL_DEVICE void gather_q8(__amdgpu_buffer_rsrc_t r, unsigned tag, int n4, int nch
       const int j = t + (k0 + k) * PT;
       if (j - lane >= n4) continue;  // wave-uniform: the whole wave is past the input
       f4 v = f4{0.f, 0.f, 0.f, 0.f};
-      if (j < n4) v = gran4_ok(a[k], b[k], tag) ? gran4_val(a[k], b[k]) : gran_wait4(r, (unsigned)j * 32u, tag, err);
+      if (j < n4) v = gran4_ok(a[k], b[k], tag) ? gran4_val(a[k], b[k]) : gran_wait4(r, (unsigned)j * 32u, tag, err, lng);
       const float m = row16_max(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
       const float scale = __fdiv_rn(m, 127.0f);
       int c0, c1, c2, c3;
@@ -497,7 +497,7 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, sign
                      const float* rmsw, float* red, float* sqa, int wave, int lane, unsigned long long* ts, F&& mid) {
   const int n4 = d.K >> 2, pad4 = Q8 ? n4 : g.nch * PL * 64;
   if (Q8 && !d.rms && d.gin) {  // Wo, W2: quantised while it is gathered
-    gather_q8<SB>(rsrc_of(d.gin), d.tag_in, n4, g.nch, xq, xsc, p.err, mid);
+    gather_q8<SB>(rsrc_of(d.gin), d.tag_in, n4, g.nch, xq, xsc, p.err, p.poll_long != 0, mid);
     if (ts && lane == 0) ts[wave == 0 ? 8 : 10] = __builtin_amdgcn_s_memrealtime();  // input gathered
     if (ts && lane == 0 && wave == 0) ts[9] = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
@@ -520,7 +520,7 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, sign
   } else {
     // every wave sweeps (the control wave alone, 16-24 loads in flight, was 1.4x slower per
     // step: the sweep is bound by loads in flight, not by the streaming waves' queued slots)
-    gather<SB, Q8>(rsrc_of(d.gin), d.tag_in, n4, pad4, threadIdx.x, PT, xs, sq, p.err, sqd, sqch, mid);
+    gather<SB, Q8>(rsrc_of(d.gin), d.tag_in, n4, pad4, threadIdx.x, PT, xs, sq, p.err, p.poll_long != 0, sqd, sqch, mid);
   }
   if (ts && lane == 0) ts[wave == 0 ? 8 : 10] = __builtin_amdgcn_s_memrealtime();  // input gathered
   float ss = 1.f;
@@ -814,8 +814,10 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
       aw.gqkv = p.gqkv; aw.gout = p.gxb;
       aw.gsc = p.gsc; aw.etab = etab;
       aw.tag_in = tb + 5u * l + 1; aw.tag_out = tb + 5u * l + 2; aw.err = p.err;
+      aw.poll_long = p.poll_long;
       return aw;
     };
+    bool pre = false;  // this block's attention unit of the coming phase has its K/V rows requested
     for (int ph = 0; ph < nph; ++ph) {
       const int l = ph / 5;
       const int kind = ph == nph - 1 ? PK_CLS : ph % 5;
@@ -833,7 +835,8 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
         } else {
           // long contexts: twice the splits, the second unit of each block on streaming wave 1
           const int units = p.H * aw.NS;
-          for (int u = blockIdx.x; u < units; u += (help ? 2 : 1) * G) attn_unit_win<HS>(aw, u, awin, lane);
+          for (int u = blockIdx.x; u < units; u += (help ? 2 : 1) * G) attn_unit_win<HS>(aw, u, awin, lane, pre);
+          pre = false;
           if (help) __syncthreads();  // the helper's window (the strip) is free for the Wo staging
         }
         TRACE(3);
@@ -844,6 +847,10 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
       stage<Q8, true>(d, g, p, xs, xq, xsc, rmsw, red, sqa, wave, lane,
                       p.trace ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots : nullptr, [] {});
       TRACE(1);
+      if constexpr (!Q8) {
+        // the coming attention unit's cached K/V rows, ahead of this block's next-phase prefetch
+        if (kind == PK_QKV && !help && p.H * p.NS <= G) pre = attn_win_preissue<HS>(attn_params(l), blockIdx.x, awin, lane);
+      }
       float2 cs0 = make_float2(1.f, 0.f);
       if (kind == PK_QKV) {
         preload_rms(p.rms_ffn + (long long)l * p.dim, p.dim, rmsw, lane);
@@ -886,6 +893,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
               aw.cnt = p.tickets + (long long)l * p.H; aw.B = 1;
               aw.gqkv = p.gqkv; aw.gout = p.gxb; aw.etab = etab;
               aw.tag_in = tb + 5u * l + 1; aw.tag_out = tb + 5u * l + 2; aw.err = p.err;
+              aw.poll_long = p.poll_long;
               for (int u = blockIdx.x + G; u < p.H * aw.NS; u += 2 * G)
                 attn_unit_win<HS>(aw, u, reinterpret_cast<float*>(xs), lane);
             }
@@ -1072,6 +1080,7 @@ bool persistent_prepare(PStep& p, int ncu, const char** why) {
   }
   if (lds_bytes(p) > kDynLdsCap) return fail("activations do not fit the LDS");
   p.attn_help = 0;
+  p.poll_long = p.dim >= 2048;
   if (!p.q8 && p.NS * 2 <= kMaxNS) {  // room for a second attention window in the strip?
     const int base = p.pad_floats, need = attn_win_floats(p.hs);
     if (base < need) p.pad_floats = need;

@@ -44,6 +44,7 @@ struct PStep {
   int attn_help;            // fp32 batch 1: the staging strip also holds an attention window, so a
                             // streaming wave runs a second attention unit per block at long contexts
   int long_ctx;             // host: launch the instantiation with that helper (persistent_long_ctx)
+  int poll_long;            // large model (dim >= 2048): input sweeps back off (common.hpp gran_backoff)
   int fault;                // test hook (THALLAMA_OPT_PERSIST_FAULT): block 0 exits at once, as
                             // if the grid were not co-resident; every other wait gives up
   int B;                    // batched step (persist_b.hip): 2..8 sequences; tok / pos / out and every
