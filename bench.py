@@ -163,6 +163,8 @@ def parse_args(argv):
     ap.add_argument("--splits", type=int, default=0)
     ap.add_argument("--no-persistent", action="store_true",
                     help="multi-launch step instead of the one-launch persistent step")
+    ap.add_argument("--persistent", action="store_true",
+                    help="the batched persistent step also for 5..8 sequences (opt-in there)")
     ap.add_argument("--no-long", action="store_true", help="skip the positions 1792..2047 line")
     ap.add_argument("--long-kernels", action="store_true",
                     help="also time each kernel class with HIP events over the long-context tail (eager replay)")
@@ -518,6 +520,8 @@ def main(argv=None):
             dec.set(tl.OPT_ATTN_SPLITS, args.splits)
         if args.no_persistent:
             dec.set(tl.OPT_PERSISTENT, 0)
+        elif args.persistent:
+            dec.set(tl.OPT_PERSISTENT, 1)
         return state, dec
 
     def launch_bytes(B, kclass, pos):

@@ -285,7 +285,7 @@ TL_DEVICE void stage_pass(const PDesc& d, const PStep& p, int q, f4* xs, float* 
       if (k4 < n4) {
         if (d.gin)
           v = gran4_ok(ga[k], gb[k], d.tag_in) ? gran4_val(ga[k], gb[k])
-                                               : gran_wait4(r, (unsigned)(b * n4 + k4) * 32u, d.tag_in, p.err);
+                                               : gran_wait4(r, (unsigned)(b * n4 + k4) * 32u, d.tag_in, p.err, p.poll_long != 0);
         else
           v = reinterpret_cast<const f4*>(p.emb + (long long)p.tok[b] * p.dim)[k4];
         if (d.rms) {
@@ -486,6 +486,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, float* res, float* xre
         aw.gqkv = p.gqkv; aw.gout = p.gxb;
         aw.etab = etab;
         aw.tag_in = tb + 5u * l + 1; aw.tag_out = tb + 5u * l + 2; aw.err = p.err;
+        aw.poll_long = p.poll_long;
         const int units = NB * p.H * p.NS;
         for (int u = blockIdx.x + G * wave; u < units; u += G * PW) attn_unit<HS, 16, true>(aw, u, lane);
         if constexpr (ROLE0) TRACE_B(3);
@@ -653,6 +654,7 @@ bool persistent_prepare_b(PStep& p, int ncu, const char** why) {
   if (ncu < 8) return fail("too few compute units");
   if ((long long)part_weight(ncu) * (p.V > p.hid ? p.V : p.hid) >= (1ll << 32)) return fail("grid x rows exceeds 32 bits");
   if (5 * p.L + 1 >= 4096) return fail("too many layers for the phase tags");
+  p.poll_long = p.dim >= 2048;  // (common.hpp gran_backoff, as persistent_prepare)
   if ((long long)p.B * (p.hid > p.dim + 2 * p.kvd ? p.hid : p.dim + 2 * p.kvd) * 32 >= (1ll << 31))
     return fail("granule offsets exceed 31 bits");
   auto owns = [&](long long n) {  // every block's share non-empty (write-after-read safety, persist.hip)
