@@ -117,6 +117,7 @@ done:
 // (device pointers), one wave each; tests/test_seqsum_gpu.py compares with the sequential chain.
 #include "seqsum.hpp"
 __global__ void __launch_bounds__(64) k_seqsum_check(const float* in, int n, float* out) {
+  tl::keep_implicit_args();  // (rocprofv3 --pmc: common.hpp)
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const float* a = in + (size_t)blockIdx.x * n;
   const int ch = tl::seqsum_ch(n);

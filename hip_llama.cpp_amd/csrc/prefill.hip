@@ -64,6 +64,7 @@ TL_DEVICE const float* wrow(const PGemmParams& p, int R) {
 // are issued before the current stage's MFMAs.
 template <int MODE>
 __global__ void __launch_bounds__(256) prefill_gemm_kernel(PGemmParams p) {
+  keep_implicit_args();  // (rocprofv3 --pmc: common.hpp)
   __shared__ __attribute__((aligned(16))) float Xs[GM_BM * GM_LD];
   __shared__ __attribute__((aligned(16))) float Ws[GM_BN * GM_LD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;

@@ -30,6 +30,7 @@ bool gemv_q8_fast_ok(const GemvParams& p) {
 // Fallback: one wave per (row, sequence), scalar, any K / GS with K % GS == 0.
 template <int MODE>
 __global__ void __launch_bounds__(256) gemv_q8_generic_kernel(GemvParams p) {
+  keep_implicit_args();  // (rocprofv3 --pmc: common.hpp)
   constexpr int RPI = RowsPerItem<MODE>::v;
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * 4 + (threadIdx.x >> 6);

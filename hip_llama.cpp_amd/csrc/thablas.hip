@@ -133,6 +133,7 @@ __global__ void __launch_bounds__(256) k_sgemm_mfma(int M, int N, int K, const f
                                                     const float* __restrict__ B, long long sbk,
                                                     long long sbj, float* __restrict__ C,
                                                     long long sci, long long scj) {
+  tl::keep_implicit_args();  // (rocprofv3 --pmc: common.hpp)
   constexpr int BM = 64, BN = 64, BK = 16;
   __shared__ float As[BK][BM + 1];
   __shared__ float Bs[BK][BN + 1];

@@ -68,6 +68,7 @@ extern "C" thablasStatus_t thaDNN_s_rmsnorm_v2_batch(thablasHandle_t* handle, in
 // ------------------------------------------------------------------ RoPE
 // reference src/thaDNN/thaDNN_rope.cpp:25-43 ; CPU src/seq.cpp:87-101
 __global__ void __launch_bounds__(256) k_rope(int dim, int head_size, int kv_dim, int pos, float* q, float* k) {
+  tl::keep_implicit_args();  // (rocprofv3 --pmc: common.hpp)
   const int i = (blockIdx.x * 256 + threadIdx.x) * 2;
   if (i >= dim) return;  // like the reference, dim is taken as even
   const int head_dim = i % head_size;
@@ -155,6 +156,7 @@ __global__ void __launch_bounds__(256) k_mha_scores(const int* pos_d, int n_head
                                                     long long att_h_stride, const float* kcache,
                                                     long long kb_stride, long long kt_stride, int head_size,
                                                     int kv_mul) {
+  tl::keep_implicit_args();  // (rocprofv3 --pmc: common.hpp)
   const int h = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int T = pos_d[b] + 1;
@@ -177,6 +179,7 @@ __global__ void __launch_bounds__(256) k_mha_av(const int* pos_d, int n_heads, f
                                                 long long att_h_stride, const float* vcache,
                                                 long long vb_stride, long long vt_stride, int head_size,
                                                 int kv_mul) {
+  tl::keep_implicit_args();  // (rocprofv3 --pmc: common.hpp)
   __shared__ float part[4][64];
   const int h = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
