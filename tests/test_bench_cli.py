@@ -60,3 +60,12 @@ def test_compare_request_file_rule():
     assert bench.compare_request_file(bad2, fx, 3)["unexplained"] == [2]
     # a missing record
     assert not bench.compare_request_file(b"3\nalpha beta gamma\n\n", fx, 3)["ok"]
+
+
+def test_parse_args_measurement_switches():
+    """The round-5 switches: the long-context per-kernel profile and the opt-in batched persistent
+    step; --prof-steps 0 (the whole headline span) stays the default."""
+    a = bench.parse_args(["--batch", "8", "--long-kernels", "--persistent"])
+    assert a.long_kernels and a.persistent and not a.no_persistent and a.batch == 8
+    d = bench.parse_args([])
+    assert not d.long_kernels and not d.persistent and d.prof_steps == 0 and d.gpus == 1
