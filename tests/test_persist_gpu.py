@@ -17,6 +17,7 @@ pytestmark = pytest.mark.gpu
 HEAD128 = (512, 1536, 2, 4, 2, 1024, 512)       # head 128, GQA (kv_dim 256)
 RAGGED = (1024, 2816, 2, 8, 8, 1024, 256)       # head 128; hidden 2816 ends mid-chunk (like 11008)
 HEAD64_GQA = (512, 1536, 3, 8, 2, 2048, 256)   # = SMALL_GQA: head 64, kv_dim 128
+WIDE = (2048, 5632, 2, 16, 4, 1024, 256)       # dim >= 2048: late granules re-polled with the back-off
 
 
 def decoder(tl, cfg, shared, seed, persistent, batch=1):
@@ -58,7 +59,7 @@ def test_profiled_as_one_class(gpu):
     assert dec.prof(gpu.K_QKV)[1] == 0
 
 
-@pytest.mark.parametrize("cfg,shared", [(SMALL, 0), (HEAD128, 0), (RAGGED, 0), (HEAD64_GQA, 0), (SMALL, 1)])
+@pytest.mark.parametrize("cfg,shared", [(SMALL, 0), (HEAD128, 0), (RAGGED, 0), (HEAD64_GQA, 0), (SMALL, 1), (WIDE, 0)])
 @pytest.mark.parametrize("graph", [0, 1])
 def test_greedy_matches_oracle(gpu, oracle, cfg, shared, graph):
     _, _, _, dec = decoder(gpu, cfg, shared, 42, 1)
@@ -76,13 +77,15 @@ def test_greedy_matches_oracle(gpu, oracle, cfg, shared, graph):
 
 
 @pytest.mark.parametrize("graph", [0, 1])
-def test_give_up_falls_back(gpu, oracle, graph):
+@pytest.mark.parametrize("cfg", [SMALL, WIDE])
+def test_give_up_falls_back(gpu, oracle, graph, cfg):
     """A persistent launch whose grid is not co-resident (simulated: block 0 missing) must not
     hang or return garbage: its bounded waits give up, the call disables the path and re-runs
-    on the multi-launch step, and the tokens still equal the oracle's."""
-    _, _, _, dec = decoder(gpu, SMALL, 0, 42, 1)
+    on the multi-launch step, and the tokens still equal the oracle's.  WIDE: the waits back off
+    to ~2000-cycle pauses (common.hpp gran_backoff), so the give-up takes longer but stays bounded."""
+    _, _, _, dec = decoder(gpu, cfg, 0, 42, 1)
     dec.set(gpu.OPT_USE_GRAPH, graph)
-    want = oracle.Model(SMALL, 0, seed=42).greedy(1, 0, 12)
+    want = oracle.Model(cfg, 0, seed=42).greedy(1, 0, 12)
     assert dec.greedy([1], [0], 4)[:, 0].tolist() == want[:4]
     assert dec.persistent()
     dec.set(gpu.OPT_PERSIST_FAULT, 1)
