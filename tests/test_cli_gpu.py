@@ -91,6 +91,24 @@ def test_test_mode_output_file_byte_identical(gpu, host, model, tmp_path, batch,
 
 
 @pytest.mark.parametrize("batch", [1, 3])
+def test_test_mode_greedy_device_or_host_argmax(gpu, host, model, tmp_path, batch):
+    """Greedy test mode (-g 1) takes each next token from the device argmax (B ids back per step)
+    unless THALLAMA_HOST_ARGMAX is set, which copies the logits back and runs the host's
+    sample_argmax like the reference (src/llama.cpp:275-286): the same output file and token count."""
+    ref, path = model
+    inp = tmp_path / "in.txt"
+    inp.write_bytes((f"{len(PROMPTS)}\n" + "\n".join(PROMPTS) + "\n").encode())
+    got = []
+    for env in ({}, {"THALLAMA_HOST_ARGMAX": "1"}):
+        out = tmp_path / f"out{len(got)}.txt"
+        r = run_cli([path, "-m", "test", "-f", str(inp), "-o", str(out), "-b", str(batch), "-g", "1", "-z", TOK],
+                    tmp_path, env=env)
+        tot = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("Total achieved token:")]
+        got.append((out.read_bytes(), tot))
+    assert got[0][0] == got[1][0] and got[0][1] == got[1][1] and got[0][1]
+
+
+@pytest.mark.parametrize("batch", [1, 3])
 def test_test_mode_worker_split_replicas(gpu, host, model, tmp_path, batch):
     """The CLI's multi-GPU form (src/llama.cpp:891-1083: one worker per GPU, each with its own
     replica and decoder, requests dealt from one shared counter), rehearsed on this GPU with
