@@ -280,15 +280,18 @@ static std::string rccl_broadcast(std::vector<Replica>& reps, int k, size_t byte
   return err;
 }
 
-// Device-to-device copies from replica 0 (hipMemcpyPeerAsync: over xGMI between GPUs, a local copy
-// when the replica shares GPU 0) into replicas [from, n).
+// Device-to-device copies into replicas [from, n), in order.  Replica r lives on device r % n_dev, so
+// replica r.dev is the first one on r's GPU: a replica past the first on its GPU copies locally from
+// it (filled already: index r.dev < r), the first replica of every other GPU copies from replica 0
+// over xGMI (hipMemcpyPeerAsync).
 static std::string peer_copies(std::vector<Replica>& reps, int from, size_t bytes) {
   for (size_t d = (size_t)from; d < reps.size(); ++d) {
     Replica& r = reps[d];
+    const Replica& src = (size_t)r.dev < d ? reps[(size_t)r.dev] : reps[0];
     hipStream_t st = nullptr;
     if (hipSetDevice(r.dev) != hipSuccess || hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess)
       return "stream creation on device " + std::to_string(r.dev);
-    hipError_t e = hipMemcpyPeerAsync(r.arena, r.dev, reps[0].arena, reps[0].dev, bytes, st);
+    hipError_t e = hipMemcpyPeerAsync(r.arena, r.dev, src.arena, src.dev, bytes, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     (void)hipStreamDestroy(st);
     if (e != hipSuccess) return std::string("hipMemcpyPeer to device ") + std::to_string(r.dev) + ": " + hipGetErrorString(e);
@@ -640,7 +643,12 @@ int main(int argc, char* argv[]) {
     // THALLAMA_PASSES=P (not in the reference; bench.py): serve the request file P times on the
     // same resident weights, one "pass i: ..." line each; the output file is the last pass's
     const char* pass_env = getenv("THALLAMA_PASSES");
-    const int passes = pass_env && atoi(pass_env) > 0 ? atoi(pass_env) : 1;
+    int passes = pass_env && atoi(pass_env) > 0 ? atoi(pass_env) : 1;
+    // THALLAMA_PASS_BUDGET_S=S (bench.py): no pass starts once the passes so far took S seconds of
+    // serving (the last pass run is then the one whose output file is written)
+    const char* budget_env = getenv("THALLAMA_PASS_BUDGET_S");
+    const double pass_budget = budget_env ? atof(budget_env) : 0.0;
+    double served_s = 0.0;
     fprintf(stderr, "\n DATA PARALLELISM \n");
     fprintf(stderr, "\n Num Devices %d\n", n_rep);
     fprintf(stderr, "\n Batch Size %d\n", batch);
@@ -681,6 +689,12 @@ int main(int argc, char* argv[]) {
       }
       if (passes > 1)
         fprintf(stdout, "pass %d: tokens %lld seconds %f\n", pass, num_gen_tokens, (double)(end - start) / 1000);
+      served_s += (double)(end - start) / 1000;
+      if (pass_budget > 0.0 && served_s >= pass_budget && pass + 1 < passes) {
+        fprintf(stdout, "pass budget: %d of %d passes in %f s (THALLAMA_PASS_BUDGET_S=%g)\n", pass + 1, passes,
+                served_s, pass_budget);
+        passes = pass + 1;
+      }
       for (int w = 0; w < n_rep; ++w)  // per GPU (worker): its tokens, requests and busy time
         fprintf(stdout, "pass %d worker %d device %d: tokens %lld requests %d seconds %f\n", pass, w, reps[w].dev,
                 w_tok[w], w_req[w], w_sec[w]);

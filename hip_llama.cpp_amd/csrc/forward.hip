@@ -147,6 +147,7 @@ struct thallama_decoder {
   float* lg_pin = nullptr;     // pinned staging of a step's logits for pageable caller buffers (logits_dst)
   const float* lg_last = nullptr;
   bool lg_last_pinned = false;
+  unsigned lg_checks = 0;      // steps since the last pointer query (re-queried every 256)
   hipEvent_t ev_stage = nullptr;  // pipeline stage done (thallama_decoder_stage)
   // layer streaming (thaDNN_s_forward_70B): the H2D copy stream and, per staging slot, layer
   // copied / layer consumed events
@@ -371,7 +372,7 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
       d->pok = tl::persistent_prepare_b(ps, d->ncu, &why);
       d->persist = batch <= kBatchPersistDefaultMax;
     } else {
-      why = batch > 8 ? "batch > 8" : "THALLAMA_BATCH_PERSIST=0";
+      why = "batch > 8";
     }
     if (!d->pok && why) d->pwhy = why;
   }
@@ -941,16 +942,33 @@ static int upload_tok_pos(thallama_decoder* d, const int* token_h, const int* po
 
 static int decoder_forward_once(thallama_decoder* d, const int* token_h, const int* pos_h, float* logits_h);
 
+// Ends the capture begun on d->stream (also after an enqueue error `e`, so the stream leaves capture
+// mode) and instantiates it into *exec; the captured graph is destroyed on every path.
+static int finish_capture(thallama_decoder* d, int e, hipGraphExec_t* exec) {
+  hipGraph_t g = nullptr;
+  hipError_t ce = hipStreamEndCapture(d->stream, &g);
+  hipError_t ie = hipSuccess;
+  if (!e && ce == hipSuccess) ie = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
+  if (g) (void)hipGraphDestroy(g);
+  if (e) return e;
+  TL_TRY(ce);
+  TL_TRY(ie);
+  return 0;
+}
+
 // Where a step's B x V logits are copied to: the caller's buffer when it is pinned (the reference
 // passes hipHostMalloc memory, src/llama.cpp:935), else the decoder's pinned staging, copied on
 // after the synchronisation — a D2H copy into pageable memory is staged by the runtime at a fraction
-// of the link rate (1 MB per step at batch 8).  The last buffer's answer is remembered.
+// of the link rate (1 MB per step at batch 8).  The answer is remembered per address and re-queried
+// every 256 steps, so a buffer freed and re-allocated at the same address as another kind of memory
+// only costs the fast path (or an extra staging copy) until then — the result is right either way.
 static float* logits_dst(thallama_decoder* d, float* logits_h) {
-  if (logits_h != d->lg_last) {
+  if (logits_h != d->lg_last || (++d->lg_checks & 255u) == 0) {
     hipPointerAttribute_t a = {};
     d->lg_last = logits_h;
-    d->lg_last_pinned = hipPointerGetAttributes(&a, logits_h) == hipSuccess && a.type == hipMemoryTypeHost;
-    (void)hipGetLastError();  // (a pageable pointer reports an error: not sticky, cleared here)
+    const hipError_t e = hipPointerGetAttributes(&a, logits_h);
+    d->lg_last_pinned = e == hipSuccess && a.type == hipMemoryTypeHost;
+    if (e != hipSuccess) (void)hipGetLastError();  // (a pageable pointer reports an error: not sticky)
   }
   if (d->lg_last_pinned) return logits_h;
   if (!d->lg_pin) {
@@ -978,14 +996,9 @@ static int decoder_forward_once(thallama_decoder* d, const int* token_h, const i
     const int lc = long_ctx(d, pos_h[0]);
     if (!d->exec_fwd[lc]) {
       ApiLock lock(api_mu());
-      hipGraph_t g = nullptr;
       TL_TRY(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
       const int e = use_persist(d) ? enqueue_persistent(d, false, lc) : enqueue_step(d);
-      hipError_t ce = hipStreamEndCapture(d->stream, &g);
-      if (e) return e;
-      TL_TRY(ce);
-      TL_TRY(hipGraphInstantiate(&d->exec_fwd[lc], g, nullptr, nullptr, 0));
-      (void)hipGraphDestroy(g);
+      if ((r = finish_capture(d, e, &d->exec_fwd[lc])) != 0) return r;
     }
     TL_TRY(hipGraphLaunch(d->exec_fwd[lc], d->stream));
   } else {
@@ -1011,7 +1024,6 @@ static int decoder_greedy_once(thallama_decoder* d, const int* token0_h, const i
 static int ensure_greedy_graph(thallama_decoder* d, int lc) {
   if (d->exec[lc]) return 0;
   ApiLock lock(api_mu());
-  hipGraph_t g = nullptr;
   TL_TRY(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
   int e = 0;
   if (use_persist(d)) {
@@ -1020,12 +1032,7 @@ static int ensure_greedy_graph(thallama_decoder* d, int lc) {
     e = enqueue_step(d);
     if (!e) e = enqueue_argmax(d);
   }
-  hipError_t ce = hipStreamEndCapture(d->stream, &g);
-  if (e) return e;
-  TL_TRY(ce);
-  TL_TRY(hipGraphInstantiate(&d->exec[lc], g, nullptr, nullptr, 0));
-  (void)hipGraphDestroy(g);
-  return 0;
+  return finish_capture(d, e, &d->exec[lc]);
 }
 
 // One greedy step with host token/pos: next_h[b] = the device argmax of slot b's logits (the

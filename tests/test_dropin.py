@@ -185,3 +185,68 @@ def test_reference_cli_timed_beside_ours(gpu, oracle, pkg, tmp_path):
     print(json.dumps(res))
     assert res["outputs_equal"]
     assert res["reference_cli_on_libthallama"]["tokens"] == res["this_cli"]["tokens"]
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_reference_cli_timed_beside_ours_7b(gpu, oracle, pkg, tmp_path):
+    """The drop-in contract priced at the size config[4] multiplies: the reference's UNCHANGED
+    src/llama.cpp test mode on libthallama.so at 8 slots on a llama2-7B-shaped v0 file — per step an
+    H2D of token/pos, thaDNN_s_forward_batch, a D2H of the 8 x 32000 logits, hipDeviceSynchronize and
+    host sampling (src/thaDNN.cpp:24-79, src/llama.cpp:1017-1050) — beside this repository's CLI in
+    the same mode (host sampling, prompts stepped like the reference: THALLAMA_NO_PREFILL=1) and with
+    its prefill, on the first 8 prompts of gen_in_64.txt.  The file's header says seq_len 256, so
+    each request runs to position 255 or BOS/EOS (the reference's test mode always runs to seq_len).
+    Same library, same decoder, same sampler: the reference's file and ours with prompts stepped
+    must be byte-identical.  Throughputs go to gpurun_out/dropin_timing_7b.json."""
+    import json
+    import time
+    if not os.path.exists(BUILT):
+        pytest.skip("oracle/_ref/llama_on_thallama not built (needs the reference tree at build time)")
+    if shutil.disk_usage(str(tmp_path)).free < 40 * 2**30:
+        pytest.skip("less than 40 GiB free for the 27 GB model file")
+    cfg = (4096, 11008, 32, 32, 32, 32000, 256)
+    path = str(tmp_path / "llama2_7b_synth_s256.bin")
+    oracle.set_threads(min(16, os.cpu_count() or 1))
+    t0 = time.perf_counter()
+    m = oracle.Model(cfg, 0, seed=20240224)
+    m.write_v0(path)
+    m.close()
+    del m
+    made_s = time.perf_counter() - t0
+    with open(os.path.join(REPO, "tests", "golden", "gen_in_64.txt"), "rb") as f:
+        lines = f.read().split(b"\n")
+    n = 8
+    inp = tmp_path / "in.txt"
+    inp.write_bytes(f"{n}\n".encode() + b"\n".join(lines[1:1 + n]) + b"\n")
+    shutil.copy(os.path.join(REPO, "tests", "golden", "tokenizer.bin"), tmp_path / "tokenizer.bin")
+    res, outs = {}, {}
+    ours = os.path.join(REPO, "build", "apps", "llama")
+    for name, exe, env in (("reference_cli_on_libthallama", BUILT, {}),
+                           ("this_cli_prompts_stepped", ours, {"THALLAMA_NO_PREFILL": "1"}),
+                           ("this_cli", ours, {})):
+        out = tmp_path / f"out_{name}.txt"
+        t1 = time.perf_counter()
+        r = subprocess.run([exe, path, "-m", "test", "-f", str(inp), "-o", str(out), "-b", "8", "-z",
+                            str(tmp_path / "tokenizer.bin")], cwd=tmp_path, capture_output=True, text=True, timeout=600,
+                           env={**os.environ, **env})
+        wall = time.perf_counter() - t1
+        assert r.returncode == 0, r.stderr[-2000:]
+        tot = [ln for ln in r.stdout.splitlines() if ln.startswith("Total achieved token:")]
+        el = [ln for ln in r.stdout.splitlines() if ln.startswith("elapsed time(s):")]
+        tokens, secs = int(tot[-1].split()[-1]), float(el[-1].split()[2].rstrip(","))
+        res[name] = {"tokens": tokens, "seconds": secs, "tok_s": round(tokens / secs, 1), "wall_s": round(wall, 2)}
+        outs[name] = out.read_bytes()
+        print(name, res[name], flush=True)
+    res["files_equal_reference_vs_stepped"] = outs["reference_cli_on_libthallama"] == outs["this_cli_prompts_stepped"]
+    res["workload"] = (f"llama2-7B-shaped fp32 v0 file (synthetic, seed 20240224, header seq_len 256), first {n} prompts "
+                       "of gen_in_64.txt, -m test -b 8 (T=1.0, top-p 0.9, the reference's per-request seed), each "
+                       "request to position 255 or BOS/EOS")
+    res["model_file_s"] = round(made_s, 1)
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", "dropin_timing_7b.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res))
+    os.remove(path)
+    assert res["files_equal_reference_vs_stepped"]
+    assert res["reference_cli_on_libthallama"]["tokens"] == res["this_cli_prompts_stepped"]["tokens"]

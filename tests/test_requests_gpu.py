@@ -7,17 +7,24 @@ the oracle's lockstep forward (bit-identical to the reference's src/seq.cpp; its
 against the reference's own 256 tokens).  Distinct prompts at distinct positions in one batch at 7B.
 
 A request's output must equal the fixture's byte for byte, except a request that reaches a near-tie
-of the CPU reference and takes the other branch there (bench.compare_request_file, the rule of
-tests/test_cli_gpu.py::test_gen_in_128_greedy_fixture): at 7B a top-2 margin under 2e-4
-(bench.REQUEST_TIE_7B: the GPU's teacher-forced drift from src/seq.cpp peaks at 1.75e-4 over 2048
-steps, the reference's own GPU path's at 5.35e-4), at most as many requests as have such a tie (9 of
-the 64).  Which requests did is printed and written under gpurun_out/.
+of the CPU reference (a top-2 margin under bench.REQUEST_TIE_7B = 2e-4: the GPU's teacher-forced drift
+from src/seq.cpp peaks at 1.75e-4 over 2048 steps) and takes the other branch there — and every such
+divergence must be PROVEN: the tie step is replayed on the GPU in this process, teacher-forced on the
+request's own history with the CLI's prefill and the same batch-8 decoder, and the GPU's argmax there
+must be the CPU's runner-up with both competing logits within 1e-4 of the CPU's (the reference's
+abs-or-rel rule, scripts/test/thaDNN.test.cpp:224-229) — the CPU's values are
+tests/golden/request_ties_llama2-7B_f32.{json,npz} (make_golden_request_ties.py, the oracle
+teacher-forced the same way).  Conversely every tie whose replay flips must have diverged in the CLI
+run (the replay predicts the CLI, a cross-process determinism check), and a step run twice in one
+process gives bitwise-identical logits.  The GPU and CPU top-2 logits of every tie step are printed and
+written under gpurun_out/.
 """
 import json
 import os
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -30,6 +37,10 @@ EXE = os.path.join(REPO, "build", "apps", "llama")
 TOK = os.path.join(REPO, "tests", "golden", "tokenizer.bin")
 FIXTURE = os.path.join(REPO, "tests", "golden", "requests_llama2-7B_f32_gen_in_64.json")
 SPEC = "synth:4096,11008,32,32,32,-32000,2048:20240224"
+TIES = os.path.join(REPO, "tests", "golden", "request_ties_llama2-7B_f32.json")
+TIE_LOGITS = os.path.join(REPO, "tests", "golden", "request_ties_llama2-7B_f32.npz")
+sys.path.insert(0, os.path.join(REPO, "tests"))
+from helpers import ref_close_mask  # noqa: E402
 
 
 @pytest.fixture(scope="module")
@@ -55,12 +66,83 @@ def run_cli(tmp_path, n, batch, env=None):
     return out.read_bytes(), r.stdout.decode()
 
 
-def check(fx, got, stdout, n, tag):
-    res = bench.compare_request_file(got, fx, n, bench.REQUEST_TIE_7B, bench.REQUEST_TIE_7B)
+def replay_ties(tl, batch, requests=None):
+    """Every tie step of the tie fixture (or those of `requests`), replayed on the GPU exactly as the CLI
+    reaches it: a `batch`-slot decoder (graphs on), the prompt's tokens 0..m-1 prefilled into the slot
+    (the scheduler's thallama_decoder_prefill call, host.cpp), then one step per position m..t fed
+    the request's own history; each case in its own slot, up to `batch` cases per pass (a slot's
+    arithmetic does not depend on its neighbours').  The tie step is then run once more and its
+    logits must be bitwise identical.  Returns [(case, gpu_logit_row)]."""
+    with open(TIES) as f:
+        tf = json.load(f)
+    rows = np.load(TIE_LOGITS)["logits"]
+    cases = [(c, rows[k]) for k, c in enumerate(tf["cases"]) if requests is None or c["request"] in requests]
+    if not cases:
+        return []
+    c = tl.Config.make(*tf["config"])
+    model = tl.DeviceModel(c, 0, seed=tf["seed"])
+    st = tl.DeviceState(c, batch)
+    dec = tl.Decoder(model, st)
+    dec.set(tl.OPT_USE_GRAPH, 1)
+    out = []
+    for g0 in range(0, len(cases), batch):
+        grp = cases[g0:g0 + batch]
+        m = [cs["prompt_tokens"] - 1 for cs, _ in grp]
+        for k, (cs, _) in enumerate(grp):
+            assert m[k] >= 1 and 1 not in cs["inputs"][1:m[k] + 1] and 2 not in cs["inputs"][1:m[k] + 1]
+            assert dec.prefill(k, cs["inputs"][:m[k]], 0) == 0
+        tmax = [cs["position"] for cs, _ in grp]
+        got = [None] * len(grp)
+        for s in range(max(t - mm for t, mm in zip(tmax, m)) + 1):
+            pos = [min(mm + s, t) for mm, t in zip(m, tmax)] + [0] * (batch - len(grp))
+            tok = [grp[k][0]["inputs"][pos[k]] for k in range(len(grp))] + [1] * (batch - len(grp))
+            lg = dec.forward(tok, pos)
+            for k in range(len(grp)):
+                if got[k] is None and pos[k] == tmax[k]:
+                    got[k] = lg[k].copy()
+        # the same step once more (the K/V rows it rewrites are the ones it wrote): bitwise the same
+        pos = tmax + [0] * (batch - len(grp))
+        tok = [grp[k][0]["inputs"][tmax[k]] for k in range(len(grp))] + [1] * (batch - len(grp))
+        again = dec.forward(tok, pos)
+        for k in range(len(grp)):
+            assert np.array_equal(again[k].view(np.uint32), got[k].view(np.uint32)), \
+                f"request {grp[k][0]['request']}: the repeated step's logits differ"
+            out.append((grp[k][0], grp[k][1], got[k]))
+    dec.close()
+    del st, model
+    return out
+
+
+def tie_evidence(replayed):
+    """{(request, position): {...}} for bench.compare_request_file: the GPU's top-2 at the tie step
+    against the CPU's, both competing logits under the 1e-4 abs-or-rel rule."""
+    ev = {}
+    for cs, cpu_row, gpu_row in replayed:
+        i0, i1 = cs["top2_ids"]
+        g = [float(gpu_row[i0]), float(gpu_row[i1])]
+        cpu = cs["top2_logits"]
+        within = bool(ref_close_mask(g, cpu, 1e-4).all())
+        ev[(cs["request"], cs["position"])] = {
+            "request": cs["request"], "position": cs["position"], "cpu_margin": cs["margin"],
+            "top2_ids": [i0, i1], "cpu_top2": cpu, "gpu_top2": g,
+            "delta": [g[0] - cpu[0], g[1] - cpu[1]], "within_tol": within,
+            "gpu_argmax": int(np.argmax(gpu_row)), "gpu_flips": int(np.argmax(gpu_row)) == i1,
+            "row_max_abs_diff": float(np.max(np.abs(gpu_row.astype(np.float64) - cpu_row))),
+            "row_beyond_rule": int((~ref_close_mask(gpu_row, cpu_row, 1e-4)).sum())}
+    return ev
+
+
+def check(fx, got, stdout, n, tag, evidence=None):
+    res = bench.compare_request_file(got, fx, n, bench.REQUEST_TIE_7B, evidence=evidence)
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     with open(os.path.join(REPO, "gpurun_out", f"requests_7b_{tag}.json"), "w") as f:
-        json.dump(res, f)
+        json.dump({**res, "evidence": list((evidence or {}).values())}, f)
     print(f"{tag}: identical {res['identical']}, diverged (request, position, top-2 margin) {res['diverged']}")
+    for d in res["diverged"]:
+        ev = (evidence or {}).get((d[0], d[1]))
+        if ev:
+            print(f"  request {d[0]} position {d[1]}: tokens {ev['top2_ids']} CPU {ev['cpu_top2']} GPU {ev['gpu_top2']} "
+                  f"delta {ev['delta']} within 1e-4 {ev['within_tol']}, GPU argmax {ev['gpu_argmax']}")
     assert not res["unexplained"], res
     assert res["ok"], res
     if res["identical"]:
@@ -71,9 +153,26 @@ def check(fx, got, stdout, n, tag):
 @pytest.mark.parametrize("batch,n", [(8, 64), (1, 16)])
 def test_gen_in_64_7b_matches_oracle_fixture(gpu, fixture, tmp_path, batch, n):
     """-b 8: all 64 prompts through the batched step (8 distinct prompts at their own positions per
-    step, prompts prefilled); -b 1: the first 16 through the persistent one-sequence step."""
+    step, prompts prefilled); -b 1: the first 16 through the persistent one-sequence step.  Every tie
+    step of the requests served is then replayed on the GPU with a decoder of the same batch."""
     got, out = run_cli(tmp_path, n, batch)
-    check(fixture, got, out, n, f"b{batch}_n{n}")
+    ev = tie_evidence(replay_ties(gpu, batch, requests=set(range(n))))
+    res = check(fixture, got, out, n, f"b{batch}_n{n}", evidence=ev)
+    for e in sorted(ev.values(), key=lambda e: e["request"]):
+        print(f"  tie: request {e['request']} position {e['position']} CPU margin {e['cpu_margin']:.3g} "
+              f"CPU {e['cpu_top2']} GPU {e['gpu_top2']} within 1e-4 {e['within_tol']} flips {e['gpu_flips']}, "
+              f"row max |d| {e['row_max_abs_diff']:.3g} ({e['row_beyond_rule']} beyond the rule)")
+        assert e["within_tol"], e  # the two competing logits of every tie step, flipped or not
+    # the replay predicts the CLI: a request whose first fixture tie the GPU flips must have diverged
+    # there (earlier ties held), and one it does not flip must not have diverged at that step
+    div = {(d[0], d[1]) for d in res["diverged"]}
+    for i in range(n):
+        steps = sorted((e["position"], e["gpu_flips"]) for e in ev.values() if e["request"] == i)
+        first_flip = next((p for p, fl in steps if fl), None)
+        if first_flip is not None:
+            assert (i, first_flip) in div, (i, first_flip, res["diverged"])
+        else:
+            assert not any(d[0] == i for d in div), (i, res["diverged"])
 
 
 def test_gen_in_64_7b_two_replicas_no_rccl(gpu, fixture, tmp_path):
