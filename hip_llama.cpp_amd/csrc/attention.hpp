@@ -156,6 +156,7 @@ struct AttnWaveParams {
   signed char* xq8;
   float* xq8s;
   int poll_long;  // persistent step of a large model: granule waits back off (common.hpp gran_backoff)
+  const unsigned* tag_seq;  // non-null: the granule tag is (*tag_seq << 12) + tag_in (qkv_attn.hip)
 };
 
 TL_DEVICE void st_sc1(float* p, float v) { st1_sc1(p, v); }
@@ -233,7 +234,10 @@ TL_DEVICE void publish_head(const AttnWaveParams& w, int b, int h, const float* 
 // kernel (persist.hip) with GR = true: q and the K/V rows at position pos come from the
 // granules the QKV phase of the same launch published (rows < pos were written by earlier
 // launches and are read from the cache), and the output is published as granules.
-template <int HS, int CH, bool GR = false>
+// GOUT: the output leaves as granules (the persistent steps) or as a plain row (store_head: the
+// multi-launch step, also when GR brings q / k_new / v_new as granules from the fused QKV +
+// attention launch, qkv_attn.hip).
+template <int HS, int CH, bool GR = false, bool GOUT = GR>
 TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
   constexpr int LPK = HS / 4;    // lanes per key row (one float4 each)
   constexpr int KPI = 64 / LPK;  // keys per wave-instruction
@@ -260,7 +264,13 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
   bool qready = false;
   // sequence b's q | k_new | v_new granules (the batched persistent step keeps B rows)
   const unsigned long long* gq = w.gqkv + (long long)b * (p.dim + 2 * p.kv_dim);
-  if constexpr (GR) rg = rsrc_of(gq);
+  // the tag to wait for: tag_in, or (*tag_seq << 12) + tag_in when the launch sequence lives in
+  // device memory (the fused multi-launch step)
+  unsigned tin = w.tag_in;
+  if constexpr (GR) {
+    rg = rsrc_of(gq);
+    if (w.tag_seq) tin += (unsigned)__builtin_amdgcn_readfirstlane((int)(w.tag_seq[0] << 12));
+  }
   else qv = reinterpret_cast<const f4*>(qrow)[lane % LPK];
   const float rs = sqrtf((float)HS);
   const bool whole = nchunks == 1;
@@ -312,23 +322,23 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
 #pragma unroll
           for (int c = 0; c < VPL; ++c) vr[c] = ld8_sc1(gq + vo / 8 + c);
         }
-        qv = gran4_ok(qa, qb, w.tag_in) ? gran4_val(qa, qb) : gran_wait4(rg, qo, w.tag_in, w.err, w.poll_long != 0);
+        qv = gran4_ok(qa, qb, tin) ? gran4_val(qa, qb) : gran_wait4(rg, qo, tin, w.err, w.poll_long != 0);
         qready = true;
         if (w.ts && lane == 0) w.ts[0] = __builtin_amdgcn_s_memrealtime();
         if (t1 == T) {
-          kn = gran4_ok(ka, kb, w.tag_in) ? gran4_val(ka, kb) : gran_wait4(rg, ko, w.tag_in, w.err, w.poll_long != 0);
+          kn = gran4_ok(ka, kb, tin) ? gran4_val(ka, kb) : gran_wait4(rg, ko, tin, w.err, w.poll_long != 0);
 #pragma unroll
           for (int c = 0; c < VPL; ++c)
-            vn[c] = (unsigned)(vr[c] >> 32) == w.tag_in ? __uint_as_float((unsigned)vr[c])
-                                                       : gran_wait(gq + vo / 8 + c, w.tag_in, w.err, w.poll_long != 0);
+            vn[c] = (unsigned)(vr[c] >> 32) == tin ? __uint_as_float((unsigned)vr[c])
+                                                       : gran_wait(gq + vo / 8 + c, tin, w.err, w.poll_long != 0);
           kvready = true;
         }
       }
       if (t1 == T) {  // this chunk holds the new row
         if (!kvready) {
-          kn = gran_wait4(rg, ko, w.tag_in, w.err, w.poll_long != 0);
+          kn = gran_wait4(rg, ko, tin, w.err, w.poll_long != 0);
 #pragma unroll
-          for (int c = 0; c < VPL; ++c) vn[c] = gran_wait(gq + vo / 8 + c, w.tag_in, w.err, w.poll_long != 0);
+          for (int c = 0; c < VPL; ++c) vn[c] = gran_wait(gq + vo / 8 + c, tin, w.err, w.poll_long != 0);
         }
         if (w.ts && lane == 0) w.ts[1] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
@@ -396,7 +406,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
   }
 
   if (whole) {
-    if constexpr (GR) {
+    if constexpr (GOUT) {
       if (w.ts && lane == 0) w.ts[2] = __builtin_amdgcn_s_memrealtime();
       publish_head<HS>(w, b, h, o, lane);
     } else {
@@ -446,7 +456,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
   }
 #pragma unroll
   for (int c = 0; c < VPL; ++c) acc[c] = __fdiv_rn(acc[c], L);
-  if constexpr (GR) {
+  if constexpr (GOUT) {
     publish_head<HS>(w, b, h, acc, lane);
   } else {
     store_head<HS>(w, b, h, acc, lane);
