@@ -2,16 +2,18 @@
 (hip_llama.cpp_amd/csrc/qkv_attn.hip, THALLAMA_OPT_FUSED_ATTN, 5..8 sequences, head size 64/128).
 
 The fused launch runs the QKV GEMV's own blocks (same tiles, splits and sums, tiles dealt per
-kv-head group) and attn_unit's multi-launch arithmetic (q and this step's k/v row arrive as
-granules instead of through the cache), so its logits must be BITWISE those of the two-launch step
-— checked at independent positions, across many 16-key chunks, with and without graphs — and the
-oracle bar of every batched path holds (greedy tokens equal the CPU decode's).  A launch whose
-waits give up (the fault hook) disables the path and the call re-runs on the two-launch step.
+kv-head group), so q / k / v are bitwise the two-launch step's; its attention units walk 16-key
+chunks (the register budget of a wave that shares the launch with the GEMV) where the stand-alone
+attention kernel walks 32, so the online-softmax merges round differently past 16 keys.  The bar is
+therefore the oracle's (the reference's src/seq.cpp forward): every logit within 1e-4 under the
+reference's abs-or-rel rule (scripts/test/thaDNN.test.cpp:224-229) at independent positions and
+across many chunks, greedy tokens equal to the CPU decode's, a step run twice bitwise identical, and
+a launch whose waits give up (the fault hook) disables the path and re-runs on the two-launch step.
 """
 import numpy as np
 import pytest
 
-from helpers import SMALL, SMALL_GQA
+from helpers import SMALL, SMALL_GQA, assert_ref_close
 
 pytestmark = pytest.mark.gpu
 
@@ -31,22 +33,32 @@ def decoder(tl, cfg, seed, batch, fused):
 @pytest.mark.parametrize("cfg", [SMALL, HEAD128, SMALL_GQA])
 @pytest.mark.parametrize("B", [5, 8])
 @pytest.mark.parametrize("graph", [0, 1])
-def test_fused_bitwise_equals_two_launches(gpu, cfg, B, graph):
-    """B sequences at their own positions, teacher-forced: every logit bitwise equal."""
-    keep_f, df = decoder(gpu, cfg, 11, B, 1)
-    keep_m, dm = decoder(gpu, cfg, 11, B, 0)
-    assert df.fused_attn() and not dm.fused_attn() and not df.persistent()
-    for d in (df, dm):
-        d.set(gpu.OPT_USE_GRAPH, graph)
+def test_fused_matches_oracle_independent_positions(gpu, oracle, cfg, B, graph):
+    """B sequences at their own positions, teacher-forced random tokens: every sequence's logits
+    within 1e-4 of its own CPU decode at every step; the last step run twice is bitwise the same."""
+    keep, dec = decoder(gpu, cfg, 11, B, 1)
+    assert dec.fused_attn() and not dec.persistent()
+    dec.set(gpu.OPT_USE_GRAPH, graph)
     rng = np.random.default_rng(B + 10 * graph)
     starts = rng.integers(0, 40, B)
     toks = rng.integers(0, cfg[5], (B, 120))
-    for step in range(70):
+    refs = [oracle.Model(cfg, 0, seed=11) for _ in range(B)]
+    for b in range(B):
+        for p in range(int(starts[b])):
+            refs[b].forward(int(toks[b, p]), p)
+    # every sequence's cache rows up to the longest prefix (a row past a sequence's own start is
+    # rewritten with the same token when its step comes)
+    for p in range(int(starts.max())):
+        dec.forward([int(toks[b, p]) for b in range(B)], [p] * B, want_logits=False)
+    for step in range(40):
         ps = [int(starts[b]) + step for b in range(B)]
         tk = [int(toks[b, ps[b]]) for b in range(B)]
-        a, m = df.forward(tk, ps), dm.forward(tk, ps)
-        assert np.array_equal(a.view(np.uint32), m.view(np.uint32)), f"step {step}"
-    assert df.fused_attn()
+        got = dec.forward(tk, ps)
+        for b in range(B):
+            assert_ref_close(got[b], refs[b].forward(tk[b], ps[b]), 1e-4, f"B={B} b={b} pos={ps[b]}")
+    again = dec.forward(tk, ps)
+    assert np.array_equal(again.view(np.uint32), got.view(np.uint32))
+    assert dec.fused_attn()
 
 
 @pytest.mark.parametrize("cfg", [SMALL, HEAD128])
@@ -61,26 +73,31 @@ def test_fused_greedy_matches_oracle(gpu, oracle, cfg):
         assert got[:, b].tolist() == oracle.Model(cfg, 0, seed=42).greedy(starts[b], 0, n), f"sequence {b}"
 
 
-def test_fused_long_context_and_prefill(gpu):
-    """Past 300 positions (19+ chunks of 16 keys, several per unit), a slot refilled by prefill (the
-    prefill chunks run unfused) among slots that keep decoding: bitwise the two-launch step."""
+def test_fused_long_context_and_prefill(gpu, oracle):
+    """Past 300 positions (19+ chunks of 16 keys, several per unit), one slot filled by prefill (the
+    prefill chunks run unfused) among slots that keep decoding: within 1e-4 of the CPU decode."""
     cfg = HEAD128
     B = 6
-    keep_f, df = decoder(gpu, cfg, 3, B, 1)
-    keep_m, dm = decoder(gpu, cfg, 3, B, 0)
+    keep, dec = decoder(gpu, cfg, 3, B, 1)
+    refs = [oracle.Model(cfg, 0, seed=3) for _ in range(B)]
     toks = np.random.default_rng(4).integers(0, cfg[5], (B, 420))
-    for d in (df, dm):
-        d.forward(toks[:, 0].tolist(), [0] * B, want_logits=False)
-        assert d.prefill(2, toks[2, :30].tolist(), 0) == 0
+    dec.forward(toks[:, 0].tolist(), [0] * B, want_logits=False)
+    for b in range(B):
+        refs[b].forward(int(toks[b, 0]), 0)
+    assert dec.prefill(2, toks[2, 1:30].tolist(), 1) == 0
+    for p in range(1, 30):
+        refs[2].forward(int(toks[2, p]), p)
     for p in range(1, 330):
         ps = [p] * B
         ps[2] = 29 + p
         tk = [int(toks[b, ps[b]]) for b in range(B)]
         want = p % 41 == 0 or p == 329
-        a, m = df.forward(tk, ps, want_logits=want), dm.forward(tk, ps, want_logits=want)
-        if want:
-            assert np.array_equal(a.view(np.uint32), m.view(np.uint32)), f"position {p}"
-    assert df.fused_attn()
+        got = dec.forward(tk, ps, want_logits=want)
+        for b in range(B):
+            r = refs[b].forward(tk[b], ps[b])
+            if want:
+                assert_ref_close(got[b], r, 1e-4, f"b={b} pos={ps[b]}")
+    assert dec.fused_attn()
 
 
 @pytest.mark.parametrize("graph", [0, 1])
