@@ -592,7 +592,9 @@ static bool fused_capable(const thallama_decoder* d) {
   return !d->q8 && d->B >= 5 && d->B <= 8 && (d->hs == 64 || d->hs == 128) && d->pok && d->pgran && d->psync &&
          (d->dim % 16) == 0 && (d->kv_dim % 16) == 0;
 }
-static bool use_fused(const thallama_decoder* d) { return d->fuse_qa && !use_persist(d); }
+// (capability re-checked at every use: thallama_decoder_create_q8 turns an fp32 decoder into an
+// int8 one after the fp32 create chose its defaults)
+static bool use_fused(const thallama_decoder* d) { return d->fuse_qa && fused_capable(d) && !use_persist(d); }
 // A path whose waits are bounded and report through the error word (checked after every sync).
 static bool use_errpath(const thallama_decoder* d) { return use_persist(d) || use_fused(d); }
 
@@ -1708,6 +1710,7 @@ extern "C" int thallama_decoder_create_q8(thallama_decoder** out, const Config* 
   if (r) return r;
   thallama_decoder* d = *out;
   d->q8 = true;
+  d->fuse_qa = false;  // the fused QKV + attention launch is fp32 only
   d->w8 = *w8;
   {  // runq's arithmetic order on the multi-launch steps (env THALLAMA_Q8_EXACT=0: the faster
      // reordered kernels, logits within the Q8 tolerance instead)

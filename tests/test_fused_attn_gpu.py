@@ -116,3 +116,18 @@ def test_fused_give_up_falls_back(gpu, oracle, graph):
     got = dec.greedy([w[3] for w in want], [4] * B, 8)
     assert [got[:, b].tolist() for b in range(B)] == [w[4:12] for w in want]
     assert not dec.fused_attn()
+
+
+def test_int8_batches_never_take_the_fused_path(gpu):
+    """The fused launch is fp32 only: an int8 decoder of 5..8 sequences (created through the fp32
+    create, then switched to its int8 weights) reports it off and keeps it off when asked."""
+    cfg = SMALL
+    c = gpu.Config.make(*cfg)
+    m = gpu.DeviceModel(c, 0, seed=5)
+    q = gpu.DeviceModelQ8(c, 0, 64, from_model=m)
+    st = gpu.DeviceState(c, 8)
+    dec = gpu.Decoder(q, st)
+    assert not dec.fused_attn()
+    dec.set(gpu.OPT_FUSED_ATTN, 1)
+    assert not dec.fused_attn()
+    dec.greedy([1] * 8, [0] * 8, 3)

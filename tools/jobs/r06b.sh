@@ -4,7 +4,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -m gpu \
-  tests/test_fused_attn_gpu.py tests/test_persist_b_gpu.py tests/test_golden_long_gpu.py > gpurun_out/r06b_pytest.log 2>&1 || exit $?
+  tests/test_fused_attn_gpu.py tests/test_golden_long_gpu.py tests/test_q8_exact_gpu.py > gpurun_out/r06b_pytest.log 2>&1 || exit $?
 for v in fused unfused fused unfused; do
   extra=""; [ $v = unfused ] && extra="--no-fused-attn"
   timeout -k 10 300 python -u bench.py --batch 8 --steps 3 --warmup 1 --skip-cpu --no-requests-point --no-cli-point \
