@@ -178,8 +178,6 @@ def parse_args(argv):
     ap.add_argument("--splits", type=int, default=0)
     ap.add_argument("--no-persistent", action="store_true",
                     help="multi-launch step instead of the one-launch persistent step")
-    ap.add_argument("--no-fused-attn", action="store_true",
-                    help="batched multi-launch step: QKV and attention as two launches (default: one, qkv_attn.hip)")
     ap.add_argument("--persistent", action="store_true",
                     help="the batched persistent step also for 5..8 sequences (opt-in there)")
     ap.add_argument("--no-long", action="store_true", help="skip the positions 1792..2047 line")
@@ -755,8 +753,6 @@ def main(argv=None):
             dec.set(tl.OPT_PERSISTENT, 0)
         elif args.persistent:
             dec.set(tl.OPT_PERSISTENT, 1)
-        if args.no_fused_attn:
-            dec.set(tl.OPT_FUSED_ATTN, 0)
         return state, dec
 
     def launch_bytes(B, kclass, pos):
@@ -1069,7 +1065,6 @@ def main(argv=None):
                         "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / step_bytes * B * world, 1)},
                 "roofline": roof,
                 "step_path": "persistent" if persistent_after else "multi-launch",
-                "fused_qkv_attention": dec.fused_attn(),
                 "persistent_fallback": bool(persistent and not persistent_after),
                 "persistent_launch": (("cooperative" if tl.lib().thallama_persistent_cooperative() else "plain")
                                       if persistent else None),

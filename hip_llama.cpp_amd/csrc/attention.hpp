@@ -156,7 +156,6 @@ struct AttnWaveParams {
   signed char* xq8;
   float* xq8s;
   int poll_long;  // persistent step of a large model: granule waits back off (common.hpp gran_backoff)
-  const unsigned* tag_seq;  // non-null: the granule tag is (*tag_seq << 12) + tag_in (qkv_attn.hip)
 };
 
 TL_DEVICE void st_sc1(float* p, float v) { st1_sc1(p, v); }
@@ -234,10 +233,7 @@ TL_DEVICE void publish_head(const AttnWaveParams& w, int b, int h, const float* 
 // kernel (persist.hip) with GR = true: q and the K/V rows at position pos come from the
 // granules the QKV phase of the same launch published (rows < pos were written by earlier
 // launches and are read from the cache), and the output is published as granules.
-// GOUT: the output leaves as granules (the persistent steps) or as a plain row (store_head: the
-// multi-launch step, also when GR brings q / k_new / v_new as granules from the fused QKV +
-// attention launch, qkv_attn.hip).
-template <int HS, int CH, bool GR = false, bool GOUT = GR>
+template <int HS, int CH, bool GR = false>
 TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
   constexpr int LPK = HS / 4;    // lanes per key row (one float4 each)
   constexpr int KPI = 64 / LPK;  // keys per wave-instruction
@@ -264,13 +260,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
   bool qready = false;
   // sequence b's q | k_new | v_new granules (the batched persistent step keeps B rows)
   const unsigned long long* gq = w.gqkv + (long long)b * (p.dim + 2 * p.kv_dim);
-  // the tag to wait for: tag_in, or (*tag_seq << 12) + tag_in when the launch sequence lives in
-  // device memory (the fused multi-launch step)
-  unsigned tin = w.tag_in;
-  if constexpr (GR) {
-    rg = rsrc_of(gq);
-    if (w.tag_seq) tin += (unsigned)__builtin_amdgcn_readfirstlane((int)(w.tag_seq[0] << 12));
-  }
+  if constexpr (GR) rg = rsrc_of(gq);
   else qv = reinterpret_cast<const f4*>(qrow)[lane % LPK];
   const float rs = sqrtf((float)HS);
   const bool whole = nchunks == 1;
@@ -322,23 +312,23 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
 #pragma unroll
           for (int c = 0; c < VPL; ++c) vr[c] = ld8_sc1(gq + vo / 8 + c);
         }
-        qv = gran4_ok(qa, qb, tin) ? gran4_val(qa, qb) : gran_wait4(rg, qo, tin, w.err, w.poll_long != 0);
+        qv = gran4_ok(qa, qb, w.tag_in) ? gran4_val(qa, qb) : gran_wait4(rg, qo, w.tag_in, w.err, w.poll_long != 0);
         qready = true;
         if (w.ts && lane == 0) w.ts[0] = __builtin_amdgcn_s_memrealtime();
         if (t1 == T) {
-          kn = gran4_ok(ka, kb, tin) ? gran4_val(ka, kb) : gran_wait4(rg, ko, tin, w.err, w.poll_long != 0);
+          kn = gran4_ok(ka, kb, w.tag_in) ? gran4_val(ka, kb) : gran_wait4(rg, ko, w.tag_in, w.err, w.poll_long != 0);
 #pragma unroll
           for (int c = 0; c < VPL; ++c)
-            vn[c] = (unsigned)(vr[c] >> 32) == tin ? __uint_as_float((unsigned)vr[c])
-                                                       : gran_wait(gq + vo / 8 + c, tin, w.err, w.poll_long != 0);
+            vn[c] = (unsigned)(vr[c] >> 32) == w.tag_in ? __uint_as_float((unsigned)vr[c])
+                                                       : gran_wait(gq + vo / 8 + c, w.tag_in, w.err, w.poll_long != 0);
           kvready = true;
         }
       }
       if (t1 == T) {  // this chunk holds the new row
         if (!kvready) {
-          kn = gran_wait4(rg, ko, tin, w.err, w.poll_long != 0);
+          kn = gran_wait4(rg, ko, w.tag_in, w.err, w.poll_long != 0);
 #pragma unroll
-          for (int c = 0; c < VPL; ++c) vn[c] = gran_wait(gq + vo / 8 + c, tin, w.err, w.poll_long != 0);
+          for (int c = 0; c < VPL; ++c) vn[c] = gran_wait(gq + vo / 8 + c, w.tag_in, w.err, w.poll_long != 0);
         }
         if (w.ts && lane == 0) w.ts[1] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
@@ -406,7 +396,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
   }
 
   if (whole) {
-    if constexpr (GOUT) {
+    if constexpr (GR) {
       if (w.ts && lane == 0) w.ts[2] = __builtin_amdgcn_s_memrealtime();
       publish_head<HS>(w, b, h, o, lane);
     } else {
@@ -456,7 +446,7 @@ TL_DEVICE void attn_unit(const AttnWaveParams& w, int unit, int lane) {
   }
 #pragma unroll
   for (int c = 0; c < VPL; ++c) acc[c] = __fdiv_rn(acc[c], L);
-  if constexpr (GOUT) {
+  if constexpr (GR) {
     publish_head<HS>(w, b, h, acc, lane);
   } else {
     store_head<HS>(w, b, h, acc, lane);

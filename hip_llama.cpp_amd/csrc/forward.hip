@@ -37,7 +37,6 @@
 #include "q8_dispatch.hpp"
 #include "persist.hpp"
 #include "prefill.hpp"
-#include "qkv_attn.hpp"
 #include "api_lock.hpp"
 
 using tl::f4;
@@ -175,7 +174,6 @@ struct thallama_decoder {
   bool profile = false;
   bool persist = true;          // requested (THALLAMA_OPT_PERSISTENT)
   bool pfault = false;          // test hook: the next persistent launch loses block 0
-  bool fuse_qa = false;         // batched multi-launch step: QKV + attention as one launch (qkv_attn.hip)
   bool pasync = false;          // an asynchronous greedy call ran persistent launches not yet checked
   // [lc]: lc = 1 is the persistent step's long-context instantiation (persistent_long_ctx)
   hipGraphExec_t exec[2] = {};      // one greedy step (step + argmax), replayed per token
@@ -209,7 +207,6 @@ struct thallama_decoder {
 
 // Options, buffers and the persistent path's state are baked into the captured graphs: drop them
 // (recaptured on next use).
-static bool fused_capable(const thallama_decoder* d);
 static void drop_graphs(thallama_decoder* d) {
   for (int i = 0; i < 2; ++i) {
     if (d->exec[i]) (void)hipGraphExecDestroy(d->exec[i]);
@@ -411,7 +408,6 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
     TL_TRY(hipMalloc(&d->pgran, sizeof(unsigned long long) * ng));
     TL_TRY(hipMemset(d->pgran, 0, sizeof(unsigned long long) * ng));
   }
-  d->fuse_qa = fused_capable(d);
   *out = d;
   return 0;
 }
@@ -466,10 +462,6 @@ extern "C" int thallama_decoder_set(thallama_decoder* d, int key, int value) {
     case THALLAMA_OPT_USE_GRAPH: d->use_graph = value != 0; break;
     case THALLAMA_OPT_PROFILE: d->profile = value != 0; break;
     case THALLAMA_OPT_PERSISTENT: d->persist = value != 0; break;
-    case THALLAMA_OPT_FUSED_ATTN:
-      d->fuse_qa = value != 0 && fused_capable(d);
-      drop_graphs(d);
-      break;
     case THALLAMA_OPT_PERSIST_FAULT:
       d->pfault = value != 0;
       drop_graphs(d);
@@ -584,65 +576,11 @@ static LayerW layer_of(const TransformerWeights& w, int l, long long dim, long l
 
 static bool use_persist(const thallama_decoder* d) { return d->persist && d->pok; }
 
-// The fused QKV + attention launch (qkv_attn.hip) of the batched multi-launch fp32 step: 5..8
-// sequences, head size 64/128; its granules live in the batched persistent step's q|k|v hand-off
-// buffer, its tags use that step's sequence word and its bounded waits that step's error word
-// (the two steps never run at once on a decoder's stream).
-static bool fused_capable(const thallama_decoder* d) {
-  return !d->q8 && d->B >= 5 && d->B <= 8 && (d->hs == 64 || d->hs == 128) && d->pok && d->pgran && d->psync &&
-         (d->dim % 16) == 0 && (d->kv_dim % 16) == 0;
-}
-// (capability re-checked at every use: thallama_decoder_create_q8 turns an fp32 decoder into an
-// int8 one after the fp32 create chose its defaults)
-static bool use_fused(const thallama_decoder* d) { return d->fuse_qa && fused_capable(d) && !use_persist(d); }
-// A path whose waits are bounded and report through the error word (checked after every sync).
-static bool use_errpath(const thallama_decoder* d) { return use_persist(d) || use_fused(d); }
-
-// Layer l's attention over io (the multi-launch step's attention launch and the fused QKV +
-// attention launch).
-static tl::AttnParams attn_params(const thallama_decoder* d, const StepIO& io, int l) {
-  tl::AttnParams a = {};
-  a.q = io.q;
-  a.kc = io.kc;
-  a.vc = io.vc;
-  a.kv_b_stride = io.kv_b_stride;
-  a.kv_l_off = (long long)l * d->S * d->kv_dim;
-  a.pos = io.pos;
-  a.out = io.xb;
-  a.part = d->part_d;
-  a.dim = d->dim;
-  a.kv_dim = d->kv_dim;
-  a.head_size = d->hs;
-  a.n_heads = d->H;
-  a.kv_mul = d->kv_mul;
-  a.seq_len = d->S;
-  a.nsplit = d->nsplit;
-  a.min_chunk = 32;
-  return a;
-}
-
-// The fused launch's q|k|v granules [B][dim + 2 kv_dim] (the batched persistent step's buffer,
-// persist_b.hip layout x | xb | hb | qkv) and the launch-sequence word (after the error word).
-static unsigned long long* fused_gqkv(const thallama_decoder* d) {
-  return d->pgran + (size_t)d->B * (2 * d->dim + d->hidden);
-}
-static unsigned* fused_seq(const thallama_decoder* d) { return d->psync + d->psync_zero + 1; }
-
 static int enqueue_step_io(thallama_decoder* d, const StepIO& io) {
   const int dim = d->dim, hid = d->hidden, kvd = d->kv_dim, S = d->S;
   const long long kv_b_stride = io.kv_b_stride;
   const TransformerWeights& w = d->w;
   d->ssq_carry = ssq_carry_ok(d) && io.nb == d->B && !io.layer_w && io.embed;
-  // the fused QKV + attention launch: the decoder's own decode step only (not prefill chunks, whose
-  // "sequences" share one cache and read rows written in the same launch, nor streamed layers)
-  bool fused = use_fused(d) && io.nb == d->B && kv_b_stride != 0 && !io.layer_w && io.embed;
-  if (fused) {
-    tl::GemvParams q = {};
-    q.n_items = (dim + 2 * kvd) / 2; q.nb = io.nb; q.K = dim; q.x_stride = dim; q.dim = dim; q.kv_dim = kvd;
-    q.head_size = d->hs; q.W0 = w.wq; q.W1 = w.wk; q.W2 = w.wv; q.x = io.x; q.y = io.q; q.kc = io.kc; q.vc = io.vc;
-    q.rope = d->rope_d; q.pos = io.pos;
-    fused = tl::qkv_attn_ok(q, d->H, d->H / d->kv_mul);
-  }
   for (int l = 0; l < d->L; ++l) {
     const long long ll = l;
     if (io.before_layer) {
@@ -680,42 +618,29 @@ static int enqueue_step_io(thallama_decoder* d, const StepIO& io) {
       p.kv_dim = kvd;
       p.head_size = d->hs;
       p.rope = d->rope_d;
-      if (fused) {
-        // 1 + 2 as ONE launch (qkv_attn.hip): the attention units read q and this step's k/v row
-        // from the granules the QKV epilogue publishes
-        p.mpart = d->mpart_d;
-        p.mcnt = d->mcnt_d;
-        p.gqkv = fused_gqkv(d);
-        p.gq_stride = dim + 2 * kvd;
-        p.gseq = fused_seq(d);
-        p.gtag = (unsigned)l + 1u;
-        tl::AttnWaveParams wp = {};
-        wp.a = attn_params(d, io, l);
-        wp.cnt = d->cnt_d;
-        wp.B = io.nb;
-        wp.NS = tl::qkv_attn_splits(io.nb, d->H, d->nsplit);
-        wp.gqkv = p.gqkv;
-        wp.tag_seq = p.gseq;
-        wp.tag_in = p.gtag;
-        if (d->pfault) {  // test hook: this launch's waits give up (a tag no epilogue writes)
-          wp.tag_seq = nullptr;
-          wp.tag_in = 0xFFFu;
-          d->pfault = false;
-        }
-        wp.err = d->psync + d->psync_zero;
-        wp.poll_long = dim >= 2048 ? 1 : 0;
-        int ev = prof_begin(d);
-        TL_TRY(tl::launch_qkv_attn(p, wp, d->stream, d->nt));
-        prof_end(d, THALLAMA_K_QKV, ev);
-      } else {
-        int ev = prof_begin(d);
-        TL_TRY(gemv(d, tl::GM_QKV, p, Q8L(wq), Q8L(wk), Q8L(wv)));
-        prof_end(d, THALLAMA_K_QKV, ev);
-      }
+      int ev = prof_begin(d);
+      TL_TRY(gemv(d, tl::GM_QKV, p, Q8L(wq), Q8L(wk), Q8L(wv)));
+      prof_end(d, THALLAMA_K_QKV, ev);
     }
     // 2. attention
-    if (!fused) {
-      const tl::AttnParams a = attn_params(d, io, l);
+    {
+      tl::AttnParams a = {};
+      a.q = io.q;
+      a.kc = io.kc;
+      a.vc = io.vc;
+      a.kv_b_stride = kv_b_stride;
+      a.kv_l_off = ll * S * kvd;
+      a.pos = io.pos;
+      a.out = io.xb;
+      a.part = d->part_d;
+      a.dim = dim;
+      a.kv_dim = kvd;
+      a.head_size = d->hs;
+      a.n_heads = d->H;
+      a.kv_mul = d->kv_mul;
+      a.seq_len = S;
+      a.nsplit = d->nsplit;
+      a.min_chunk = 32;
       const int lpk = d->hs / 4;
       const size_t lds = 64 + (size_t)(S > 1024 ? S : 1024) * 4;
       int ev = prof_begin(d);
@@ -844,7 +769,6 @@ static int enqueue_step_io(thallama_decoder* d, const StepIO& io) {
     TL_TRY(gemv(d, tl::GM_STORE, p, d->q8 ? d->w8.wcls : nullptr, nullptr, nullptr));
     prof_end(d, THALLAMA_K_CLS, ev);
   }
-  if (fused) TL_TRY(tl::launch_step_seq_advance(fused_seq(d), d->stream));  // this step's tags are spent
   return 0;
 }
 
@@ -913,7 +837,7 @@ constexpr int kPersistFellBack = (int)hipErrorLaunchFailure;
 // Enqueued on d->stream after a call's persistent launches, before its synchronisation: the
 // error word lands in pinned host memory with the rest of the call (no legacy-stream copy).
 static int enqueue_err_read(thallama_decoder* d) {
-  if (d->psync && use_errpath(d)) {
+  if (d->psync && use_persist(d)) {
     TL_TRY(hipMemcpyAsync(d->perr_h, d->psync + d->psync_zero, sizeof(unsigned), hipMemcpyDeviceToHost, d->stream));
     d->err_pending = true;
   }
@@ -929,17 +853,7 @@ static int check_persist(thallama_decoder* d) {
   TL_TRY(hipMemsetAsync(d->psync, 0, sizeof(unsigned) * (d->psync_zero + 32), d->stream));
   TL_TRY(hipMemsetAsync(d->cnt_d, 0, sizeof(unsigned) * (size_t)d->B * d->H, d->stream));
   TL_TRY(hipStreamSynchronize(d->stream));
-  if (!use_persist(d) && use_fused(d)) {
-    d->fuse_qa = false;  // the fused QKV + attention launch gave up: the two-launch step from now on
-    {
-      ApiLock lock(api_mu());
-      drop_graphs(d);
-    }
-    g_last_error = "fused QKV + attention: a granule wait timed out; path disabled";
-    return kPersistFellBack;
-  }
   d->pok = false;
-  d->fuse_qa = false;  // (it shares the persistent step's buffers)
   d->pwhy = "a grid barrier timed out";
   {
     ApiLock lock(api_mu());
@@ -950,7 +864,6 @@ static int check_persist(thallama_decoder* d) {
 }
 
 extern "C" int thallama_decoder_persistent(thallama_decoder* d) { return d && use_persist(d) ? 1 : 0; }
-extern "C" int thallama_decoder_fused_attn(thallama_decoder* d) { return d && use_fused(d) ? 1 : 0; }
 extern "C" int thallama_persistent_cooperative(void) { return tl::persistent_cooperative() ? 1 : 0; }
 
 // Diagnostics: copy the persistent step's hand-off granules {value, tag} (x | xb | hb | q k v |
@@ -1069,8 +982,9 @@ static float* logits_dst(thallama_decoder* d, float* logits_h) {
 }
 
 extern "C" int thallama_decoder_forward(thallama_decoder* d, const int* token_h, const int* pos_h, float* logits_h) {
+  const bool persistent = d && use_persist(d);
   int r = decoder_forward_once(d, token_h, pos_h, logits_h);
-  for (int retry = 0; retry < 2 && r == kPersistFellBack; ++retry) r = decoder_forward_once(d, token_h, pos_h, logits_h);
+  if (r == kPersistFellBack && persistent && !use_persist(d)) r = decoder_forward_once(d, token_h, pos_h, logits_h);
   return r;
 }
 
@@ -1145,8 +1059,9 @@ static int decoder_step_argmax_once(thallama_decoder* d, const int* token_h, con
 }
 
 extern "C" int thallama_decoder_step_argmax(thallama_decoder* d, const int* token_h, const int* pos_h, int* next_h) {
+  const bool persistent = d && use_persist(d);
   int r = decoder_step_argmax_once(d, token_h, pos_h, next_h);
-  for (int retry = 0; retry < 2 && r == kPersistFellBack; ++retry) r = decoder_step_argmax_once(d, token_h, pos_h, next_h);
+  if (r == kPersistFellBack && persistent && !use_persist(d)) r = decoder_step_argmax_once(d, token_h, pos_h, next_h);
   return r;
 }
 
@@ -1160,8 +1075,9 @@ extern "C" int thallama_decoder_argmax_cb(void* ctx, int worker, int batch, cons
 
 extern "C" int thallama_decoder_greedy(thallama_decoder* d, const int* token0_h, const int* pos0_h, int n_steps,
                                        int* tokens_out_h, int sync) {
+  const bool persistent = d && use_persist(d);
   int r = decoder_greedy_once(d, token0_h, pos0_h, n_steps, tokens_out_h, sync);
-  for (int retry = 0; retry < 2 && r == kPersistFellBack; ++retry)
+  if (r == kPersistFellBack && persistent && !use_persist(d))
     r = decoder_greedy_once(d, token0_h, pos0_h, n_steps, tokens_out_h, sync);
   return r;
 }
@@ -1207,7 +1123,7 @@ static int decoder_greedy_once(thallama_decoder* d, const int* token0_h, const i
   } else if (sync) {
     TL_TRY(hipStreamSynchronize(d->stream));
   } else {
-    d->pasync = d->pasync || (n_steps > 0 && use_errpath(d));
+    d->pasync = d->pasync || (n_steps > 0 && use_persist(d));
     prof_collect(d);
     return 0;
   }
@@ -1710,7 +1626,6 @@ extern "C" int thallama_decoder_create_q8(thallama_decoder** out, const Config* 
   if (r) return r;
   thallama_decoder* d = *out;
   d->q8 = true;
-  d->fuse_qa = false;  // the fused QKV + attention launch is fp32 only
   d->w8 = *w8;
   {  // runq's arithmetic order on the multi-launch steps (env THALLAMA_Q8_EXACT=0: the faster
      // reordered kernels, logits within the Q8 tolerance instead)

@@ -86,15 +86,6 @@ struct GemvParams {
   float* ssq_out;
   const float* ssq_in;
   int ssq_nt;            // tiles of the producing launch (its rows / 16)
-  // fused QKV + attention launch (qkv_attn.hip), QKV only: the epilogue also publishes every row
-  // pair as two {value, tag} granules into gqkv[b * gq_stride + row] (q | k_new | v_new), tag =
-  // (*gseq << 12) + gtag; and tile slots are dealt in kv-head groups (tperm_kv_mul > 0: each kv
-  // head's q tiles (kv_mul heads), then its k tiles, then its v tiles) so a head completes early
-  unsigned long long* gqkv;
-  long long gq_stride;
-  const unsigned* gseq;
-  unsigned gtag;
-  int tperm_kv_mul;
 };
 
 // Blocks the matrix-core GEMV aims for: 4 per CU (6 and 8 lost 12-15% everywhere, 2 wins only for

@@ -57,9 +57,6 @@ TL_DEVICE void epi_one(const GemvParams& p, int item, int b, float v0, float v1)
       const float r1 = __fadd_rn(__fmul_rn(a0, cs.y), __fmul_rn(a1, cs.x));
       a0 = r0; a1 = r1;
     }
-    if (p.gqkv)  // the fused launch's attention waves read q / k_new / v_new from these granules
-      st_gran2(rsrc_of(p.gqkv), (unsigned)(((long long)b * p.gq_stride + row) * 8), (p.gseq[0] << 12) + p.gtag, a0,
-               a1);
     if (row < p.dim) {
       float* qd = p.y + (long long)b * p.y_stride + row;
       qd[0] = a0; qd[1] = a1;
@@ -115,21 +112,9 @@ __global__ void __launch_bounds__(256) gemv_prenorm_kernel(GemvParams p) {
 // r01_mfma_sweep.jsonl); LDS traffic is ~1 B per weight byte.  The weights of group g + 1
 // are in flight while group g multiplies; steps past the run load a clamped (valid)
 // address and multiply zero activations, so no load is predicated.
-// Tile slot -> tile of the fused QKV launch: slots dealt in kv-head groups (q tiles of the group's
-// kv_mul heads, then its k tiles, then its v tiles), so the tiles of one head finish together.
-TL_DEVICE int qkv_tile_of_slot(const GemvParams& p, int slot) {
-  const int th = p.head_size >> 4;       // tiles per head
-  const int tq = p.tperm_kv_mul * th;    // q tiles per group
-  const int g = slot / (tq + 2 * th), j = slot - g * (tq + 2 * th);
-  if (j < tq) return g * tq + j;
-  if (j < tq + th) return (p.dim >> 4) + g * th + (j - tq);
-  return (p.dim >> 4) + (p.kv_dim >> 4) + g * th + (j - tq - th);
-}
-
-// The body of one block of gemv_mfma_kernel, for block index bid (the fused QKV + attention
-// launch, qkv_attn.hip, runs it in its first blocks).
 template <int MODE, bool NT, int XI>
-TL_DEVICE void gemv_mfma_block(const GemvParams& p, int bid) {
+__global__ void __launch_bounds__(kMfmaWaves * 64) gemv_mfma_kernel(GemvParams p) {
+  keep_implicit_args();
   constexpr int W = kMfmaWaves;
   constexpr bool TWO = MODE == GM_SWIGLU;
   constexpr int NR = TWO ? 2 : 1;      // weight tiles per group; tile NR is the activations
@@ -151,8 +136,7 @@ TL_DEVICE void gemv_mfma_block(const GemvParams& p, int bid) {
   const int lr = lane / LPR, lc = lane % LPR;  // load map: row RPI v + lr, 16-B chunk lc
   const int K = p.K, nb = p.nb;
   const long long Kl = K;
-  const int slot = bid / p.msplit, split = bid - slot * p.msplit;
-  const int tile = MODE == GM_QKV && p.tperm_kv_mul ? qkv_tile_of_slot(p, slot) : slot;
+  const int tile = blockIdx.x / p.msplit, split = blockIdx.x - tile * p.msplit;
   const int n_rows = MODE == GM_QKV ? 2 * p.n_items : p.n_items;
 
   const float* wrow[NR][NI];
@@ -352,12 +336,6 @@ TL_DEVICE void gemv_mfma_block(const GemvParams& p, int bid) {
     }
   }
   if (msplit > 1 && threadIdx.x == 0) __hip_atomic_store(p.mcnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int MODE, bool NT, int XI>
-__global__ void __launch_bounds__(kMfmaWaves * 64) gemv_mfma_kernel(GemvParams p) {
-  keep_implicit_args();
-  gemv_mfma_block<MODE, NT, XI>(p, blockIdx.x);
 }
 
 }  // namespace tl

@@ -91,7 +91,7 @@ STATUS = {0: "SUCCESS", 1: "NOT_INITIALIZED", 2: "ALLOC_FAILED", 3: "INVALID_VAL
 # kernel classes (include/thallama.h)
 K_QKV, K_ATTN, K_WO, K_FFN_UP, K_FFN_DOWN, K_CLS, K_ARGMAX, K_STEP = range(8)
 K_NAMES = ["qkv", "attn", "wo", "ffn_up", "ffn_down", "cls", "argmax", "step"]
-OPT_NT_WEIGHTS, OPT_ATTN_SPLITS, OPT_USE_GRAPH, OPT_PROFILE, OPT_PERSISTENT, OPT_PERSIST_FAULT, OPT_FUSED_ATTN = 1, 2, 3, 4, 5, 6, 7
+OPT_NT_WEIGHTS, OPT_ATTN_SPLITS, OPT_USE_GRAPH, OPT_PROFILE, OPT_PERSISTENT, OPT_PERSIST_FAULT = 1, 2, 3, 4, 5, 6
 
 _lib = None
 
@@ -154,7 +154,6 @@ def lib():
             "thallama_decoder_destroy": (None, [VP]),
             "thallama_decoder_set": (I, [VP, I, I]),
             "thallama_decoder_persistent": (I, [VP]),
-            "thallama_decoder_fused_attn": (I, [VP]),
             "thallama_persistent_cooperative": (I, []),
             "thallama_decoder_granules": (I, [VP, C.POINTER(C.c_ulonglong), S]),
             "thallama_decoder_prefill": (I, [VP, I, c_int_p, I, I]),
@@ -434,10 +433,6 @@ class Decoder:
     def persistent(self):
         """True if steps run as one persistent launch (persist.hip)."""
         return bool(lib().thallama_decoder_persistent(self.h))
-
-    def fused_attn(self):
-        """True if multi-launch steps run QKV + attention as one launch (qkv_attn.hip)."""
-        return bool(lib().thallama_decoder_fused_attn(self.h))
 
     def ptrace(self, enable=True):
         """Enable the persistent-step timeline; returns the stamps of the last launch as a

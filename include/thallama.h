@@ -39,15 +39,8 @@ enum {
   THALLAMA_OPT_PERSIST_FAULT = 6,  /* test hook: the next persistent launch runs without its
                                     block 0 (as if the grid were not co-resident): its waits
                                     give up, the call disables the path and re-runs on the
-                                    multi-launch step (also the fused launch below). */
-  THALLAMA_OPT_FUSED_ATTN = 7,   /* 0/1: the batched multi-launch fp32 step (5..8 sequences, head
-                                    size 64/128) runs RMSNorm + QKV + RoPE + K/V write and the
-                                    attention as ONE launch (qkv_attn.hip).  Default 1 where
-                                    supported; profiled as THALLAMA_K_QKV (no THALLAMA_K_ATTN). */
+                                    multi-launch step. */
 };
-
-/* 1 if the decoder's multi-launch steps run the fused QKV + attention launch, else 0. */
-int thallama_decoder_fused_attn(thallama_decoder* d);
 
 /* 1 if the decoder runs its steps as one persistent launch (THALLAMA_OPT_PERSISTENT
  * requested and the shape supported), else 0. */
