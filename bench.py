@@ -302,7 +302,7 @@ def cli_passes(stdout):
     return runs
 
 
-def cli_serve(args, world, B, passes, warmup, budget_s=0.0, devices=None):
+def cli_serve(args, world, B, passes, warmup, budget_s=0.0, devices=None, replicas=None):
     """One run of the drop-in CLI (build/apps/llama, app/run.cpp — the reference's
     test_data_parallelism, src/llama.cpp:891-1083: one host thread per GPU, B slots per thread, one
     weight image made on GPU 0 and RCCL-broadcast over xGMI) serving the first prompts_per_gpu x N
@@ -311,7 +311,11 @@ def cli_serve(args, world, B, passes, warmup, budget_s=0.0, devices=None):
     a child process over GPUs 0..N-1; it serves the file warmup + passes times on the same
     resident weights (THALLAMA_PASSES).  Returns tokens / serve time of the timed passes (the CLI's
     own clock, weights already in HBM) and whether the output file equals the committed
-    one-process fixture of B slots, byte for byte."""
+    one-process fixture of B slots, byte for byte.  budget_s > 0: no pass starts after budget_s
+    seconds of serving (THALLAMA_PASS_BUDGET_S), so the run's wall time is bounded whatever a pass
+    costs; the passes actually timed are reported.  devices: HIP_VISIBLE_DEVICES for the child
+    (default: GPUs 0..world-1 unless the environment already restricts them); replicas: workers
+    (THALLAMA_REPLICAS; default --cli-replicas, 0 = one per GPU)."""
     cfg_t, shared, mname = MODELS[args.model]
     q8 = args.dtype == "int8"
     T = args.decode_len
@@ -333,8 +337,11 @@ def cli_serve(args, world, B, passes, warmup, budget_s=0.0, devices=None):
         env["HIP_VISIBLE_DEVICES"] = devices
     elif "HIP_VISIBLE_DEVICES" not in env and "ROCR_VISIBLE_DEVICES" not in env:
         env["HIP_VISIBLE_DEVICES"] = ",".join(str(i) for i in range(world))
-    if args.cli_replicas:
-        env["THALLAMA_REPLICAS"] = str(args.cli_replicas)
+    reps = args.cli_replicas if replicas is None else replicas
+    if reps:
+        env["THALLAMA_REPLICAS"] = str(reps)
+    else:
+        env.pop("THALLAMA_REPLICAS", None)
     env["THALLAMA_PASSES"] = str(warmup + passes)
     if budget_s > 0:
         env["THALLAMA_PASS_BUDGET_S"] = str(budget_s)
@@ -390,7 +397,7 @@ def cli_serve(args, world, B, passes, warmup, budget_s=0.0, devices=None):
             "cmd": " ".join(os.path.relpath(c, REPO) if c.startswith(REPO) else c for c in cmd),
             "passes": [{"tokens": t, "seconds": x} for t, x in runs], "warmup_passes": warmup,
             "pass_budget_s": budget_s, "pass_budget_hit": budget_hit[0] if budget_hit else None,
-            "load_s": load, "wall_s": round(wall, 2), "replicas": args.cli_replicas or world,
+            "load_s": load, "wall_s": round(wall, 2), "replicas": reps or world,
             "visible_devices": env.get("HIP_VISIBLE_DEVICES", env.get("ROCR_VISIBLE_DEVICES")),
             "output_matches_fixture": check["identical"] if check else None,
             "fixture_check": check,
@@ -493,7 +500,7 @@ def cli_run(args, world, rank):
         # the same per-GPU job on GPU 0 alone, in this run: the 1-GPU end of the weak-scaling curve
         one = None
         if world > 1 and not args.no_scaling_point:
-            one = cli_serve(args, 1, B, 3, 1, budget_s=args.cli_budget / 4, devices=_first_device())
+            one = cli_serve(args, 1, B, 3, 1, budget_s=args.cli_budget / 4, devices=_first_device(), replicas=0)
         prompts = read_prompts(PROMPTS, r["prompts"])
         from hip_llama_cpp_amd import host as H
         tok = H.Tokenizer(TOKENIZER)
