@@ -496,6 +496,15 @@ template <bool Q8, bool ROLE0, class F>
 TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, signed char* xq, float* xsc,
                      const float* rmsw, float* red, float* sqa, int wave, int lane, unsigned long long* ts, F&& mid) {
   const int n4 = d.K >> 2, pad4 = Q8 ? n4 : g.nch * PL * 64;
+#ifdef PERSIST_DIAG_NO_GATHER
+  // traffic-attribution build only (tools/build_variant.sh; profiles/r06/handoff_traffic_bisect.txt):
+  // the phase input is not gathered — wrong results; what the rest of the step reads is the point
+  if (d.gin) {
+    mid();
+    __syncthreads();
+    return;
+  }
+#endif
   if (Q8 && !d.rms && d.gin) {  // Wo, W2: quantised while it is gathered
     gather_q8<SB>(rsrc_of(d.gin), d.tag_in, n4, g.nch, xq, xsc, p.err, p.poll_long != 0, mid);
     if (ts && lane == 0) ts[wave == 0 ? 8 : 10] = __builtin_amdgcn_s_memrealtime();  // input gathered
