@@ -498,8 +498,10 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, sign
   const int n4 = d.K >> 2, pad4 = Q8 ? n4 : g.nch * PL * 64;
 #ifdef PERSIST_DIAG_NO_GATHER
   // traffic-attribution build only (tools/build_variant.sh; profiles/r06/handoff_traffic_bisect.txt):
-  // the phase input is not gathered — wrong results; what the rest of the step reads is the point
-  if (d.gin) {
+  // the Wo and W2 phases do not gather their input (xb, hb) — wrong results; what the rest of the
+  // step reads is the point.  The normed phases (QKV, W1/W3) still gather x from every block, so
+  // every hand-off buffer is still rewritten only after all its readers are done.
+  if (d.gin && !d.rms) {
     mid();
     __syncthreads();
     return;
