@@ -598,6 +598,9 @@ TL_DEVICE void stage(const PDesc& d, const PGeo& g, const PStep& p, f4* xs, sign
 // Control wave, while the others stream: the next norm's weights into LDS (constants; only
 // the staging reads rmsw, and it has finished).
 TL_DEVICE void preload_rms(const float* w, int dim, float* rmsw, int lane) {
+#ifdef PERSIST_DIAG_NO_RMSW  // traffic-attribution build only (as PERSIST_DIAG_NO_GATHER): no preload
+  return;
+#endif
   const f4* s4 = reinterpret_cast<const f4*>(w);
   f4* d4 = reinterpret_cast<f4*>(rmsw);
   for (int j = lane; j < (dim >> 2); j += 64) d4[j] = s4[j];

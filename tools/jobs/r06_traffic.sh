@@ -10,7 +10,7 @@ L=hip_llama.cpp_amd/lib
 cp $L/libthallama.so $L/libthallama.so.keep
 B="python bench.py --skip-cpu --no-long --no-requests-point --no-cli-point --steps 1 --warmup 0 --decode-len 8"
 rc=0
-for v in base nogather; do
+for v in ${VARIANTS:-base nogather}; do
   cp $L/libthallama.so.$v $L/libthallama.so
   for dt in f32 int8; do
     for c in FETCH_SIZE WRITE_SIZE; do
