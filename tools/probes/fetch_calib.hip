@@ -52,6 +52,19 @@ __global__ void __launch_bounds__(NT) k8s(const char* W, unsigned* out) {
   out[blockIdx.x * NT + threadIdx.x] = a;
 }
 
+// write-through (sc1) stores of the hand-off shapes over 64 MiB: do they cause memory-side READS?
+//   kst8  : one 8-B sc1 store per lane, a wave's 512 B contiguous   (the {value, tag} granules)
+//   kst16 : one 16-B sc1 store per lane, a wave's 1 KiB contiguous  (two granules: st_gran2)
+constexpr size_t SBYTES = 64ull << 20;
+__global__ void __launch_bounds__(NT) kst8(char* D) {
+  const size_t i = ((size_t)blockIdx.x * NT + threadIdx.x) * 8u;
+  if (i < SBYTES) __builtin_amdgcn_raw_buffer_store_b64(v2u{(unsigned)i, 1u}, __builtin_amdgcn_make_buffer_rsrc(D, (short)0, 0x7ffffff0, 0x00020000), (unsigned)i, 0, 16);
+}
+__global__ void __launch_bounds__(NT) kst16(char* D) {
+  const size_t i = ((size_t)blockIdx.x * NT + threadIdx.x) * 16u;
+  if (i < SBYTES) __builtin_amdgcn_raw_buffer_store_b128(v4u{(unsigned)i, 1u, 2u, 3u}, __builtin_amdgcn_make_buffer_rsrc(D, (short)0, 0x7ffffff0, 0x00020000), (unsigned)i, 0, 16);
+}
+
 int main() {
   char* W;
   unsigned* out;
@@ -69,7 +82,16 @@ int main() {
     hipLaunchKernelGGL(k16e, dim3((1u << 30) / SLICE), dim3(NT), 0, 0, (const char*)E, out);
     hipLaunchKernelGGL(k8s, dim3(NB), dim3(NT), 0, 0, (const char*)W, out);
   }
+  char* D;
+  CK(hipMalloc(&D, SBYTES));
+  CK(hipMemset(D, 0, SBYTES));
+  for (int rep = 0; rep < 2; ++rep) {
+    hipLaunchKernelGGL(k16e, dim3((1u << 30) / SLICE), dim3(NT), 0, 0, (const char*)E, out);
+    hipLaunchKernelGGL(kst8, dim3((unsigned)(SBYTES / 8 / NT)), dim3(NT), 0, 0, D);
+    hipLaunchKernelGGL(k16e, dim3((1u << 30) / SLICE), dim3(NT), 0, 0, (const char*)E, out);
+    hipLaunchKernelGGL(kst16, dim3((unsigned)(SBYTES / 16 / NT)), dim3(NT), 0, 0, D);
+  }
   CK(hipDeviceSynchronize());
-  printf("fetch_calib: %zu bytes per k16 / k4 / k8s launch (k16 over 1 GiB between them: cold caches)\n", BYTES);
+  printf("fetch_calib: %zu bytes per k16 / k4 / k8s launch, %zu written per kst8 / kst16 launch (k16e over 1 GiB between them: cold caches)\n", BYTES, SBYTES);
   return 0;
 }
