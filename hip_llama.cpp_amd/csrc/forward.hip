@@ -187,6 +187,9 @@ struct thallama_decoder {
   const signed char* pq8w[7] = {};       // int8: layer-0 int8 block of wq wk wv wo w1 w2 w3
   long long pq8ls[7] = {};                // and the byte stride between layers
   bool pok = false;             // shape supported
+  bool pk = false;              // 8 sequences: the K-split persistent step is supported (persist_k.hip)
+  bool ksplit = true;           //   and requested (THALLAMA_OPT_KSPLIT)
+  unsigned long long* pkgran = nullptr;  // its hand-off area
   unsigned long long* ptrace = nullptr;  // optional timeline of the persistent step
   size_t ptrace_n = 0;
   // batched prompt processing (prefill.hip) for kPrefillChunk tokens, allocated at creation
@@ -371,6 +374,17 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
     } else if (batch <= 8) {
       d->pok = tl::persistent_prepare_b(ps, d->ncu, &why);
       d->persist = batch <= kBatchPersistDefaultMax;
+      if (batch == 8) {  // the K-split step (persist_k.hip): the default at 8 sequences
+        tl::PStep pk = ps;
+        const char* kwhy = nullptr;
+        d->pk = tl::persistent_prepare_k(pk, d->ncu, &kwhy);
+        const char* ev = getenv("THALLAMA_KSPLIT");
+        d->ksplit = !(ev && ev[0] == '0');
+        if (d->pk) {
+          d->pok = true;
+          d->persist = d->ksplit;
+        }
+      }
     } else {
       why = "batch > 8";
     }
@@ -407,6 +421,13 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
     const size_t ng = granule_count(d);
     TL_TRY(hipMalloc(&d->pgran, sizeof(unsigned long long) * ng));
     TL_TRY(hipMemset(d->pgran, 0, sizeof(unsigned long long) * ng));
+  }
+  if (d->pk) {
+    tl::PStep ps = {};
+    ps.dim = d->dim; ps.hid = d->hidden; ps.kvd = d->kv_dim; ps.V = d->V;
+    const size_t nk = (size_t)tl::persistent_k_granules(ps, d->ncu);
+    TL_TRY(hipMalloc(&d->pkgran, sizeof(unsigned long long) * nk));
+    TL_TRY(hipMemset(d->pkgran, 0, sizeof(unsigned long long) * nk));
   }
   *out = d;
   return 0;
@@ -446,6 +467,7 @@ extern "C" void thallama_decoder_destroy(thallama_decoder* d) {
   (void)hipFree(d->psync);
   (void)hipFree(d->pbmax);
   (void)hipFree(d->pgran);
+  (void)hipFree(d->pkgran);
   (void)hipFree(d->ptrace);
   for (void* b : {(void*)d->pf_att, (void*)d->pf_x, (void*)d->pf_xn, (void*)d->pf_q, (void*)d->pf_xb, (void*)d->pf_hb,
                   (void*)d->pf_part, (void*)d->pf_cnt, (void*)d->pf_tok, (void*)d->pf_pos})
@@ -462,6 +484,7 @@ extern "C" int thallama_decoder_set(thallama_decoder* d, int key, int value) {
     case THALLAMA_OPT_USE_GRAPH: d->use_graph = value != 0; break;
     case THALLAMA_OPT_PROFILE: d->profile = value != 0; break;
     case THALLAMA_OPT_PERSISTENT: d->persist = value != 0; break;
+    case THALLAMA_OPT_KSPLIT: d->ksplit = value != 0; break;
     case THALLAMA_OPT_PERSIST_FAULT:
       d->pfault = value != 0;
       drop_graphs(d);
@@ -575,6 +598,9 @@ static LayerW layer_of(const TransformerWeights& w, int l, long long dim, long l
 }
 
 static bool use_persist(const thallama_decoder* d) { return d->persist && d->pok; }
+// The persistent step at 8 sequences is the K-split one (persist_k.hip) unless THALLAMA_OPT_KSPLIT
+// is 0 (then persist_b.hip, if that shape check passed).
+static bool use_ksplit(const thallama_decoder* d) { return use_persist(d) && d->pk && d->ksplit; }
 
 static int enqueue_step_io(thallama_decoder* d, const StepIO& io) {
   const int dim = d->dim, hid = d->hidden, kvd = d->kv_dim, S = d->S;
@@ -816,13 +842,17 @@ static int enqueue_persistent(thallama_decoder* d, bool argmax, int lc) {
     p.scls = d->w8.wcls->s;
   }
   const char* why = nullptr;
-  if (!(d->B > 1 ? tl::persistent_prepare_b(p, d->ncu, &why) : tl::persistent_prepare(p, d->ncu, &why))) {
+  const bool ks = use_ksplit(d);
+  p.gk = ks ? d->pkgran : nullptr;
+  if (!(ks ? tl::persistent_prepare_k(p, d->ncu, &why)
+           : d->B > 1 ? tl::persistent_prepare_b(p, d->ncu, &why) : tl::persistent_prepare(p, d->ncu, &why))) {
     g_last_error = std::string("persistent step: ") + (why ? why : "unsupported");
     return (int)hipErrorInvalidValue;
   }
   TL_TRY(hipMemsetAsync(p.sync, 0, sizeof(unsigned) * d->psync_zero, d->stream));
   const int ev = prof_begin(d);
-  TL_TRY(d->B > 1 ? tl::launch_persistent_step_b(p, d->stream, d->ncu) : tl::launch_persistent_step(p, d->stream, d->ncu));
+  TL_TRY(ks ? tl::launch_persistent_step_k(p, d->stream, d->ncu)
+            : d->B > 1 ? tl::launch_persistent_step_b(p, d->stream, d->ncu) : tl::launch_persistent_step(p, d->stream, d->ncu));
   prof_end(d, THALLAMA_K_STEP, ev);
   return 0;
 }
@@ -864,6 +894,7 @@ static int check_persist(thallama_decoder* d) {
 }
 
 extern "C" int thallama_decoder_persistent(thallama_decoder* d) { return d && use_persist(d) ? 1 : 0; }
+extern "C" int thallama_decoder_ksplit(thallama_decoder* d) { return d && use_ksplit(d) ? 1 : 0; }
 extern "C" int thallama_persistent_cooperative(void) { return tl::persistent_cooperative() ? 1 : 0; }
 
 // Diagnostics: copy the persistent step's hand-off granules {value, tag} (x | xb | hb | q k v |
@@ -1647,8 +1678,11 @@ extern "C" int thallama_decoder_create_q8(thallama_decoder** out, const Config* 
     TL_TRY(hipMalloc(&d->xq_d, 8 * kmax));
     TL_TRY(hipMalloc(&d->xqs_d, sizeof(float) * 8 * (kmax / 16 + 1)));
   }
-  if (batch > 1 && d->pok) {  // the batched persistent step is fp32 only: int8 batches run multi-launch
+  if (batch > 1 && d->pok) {  // the batched persistent steps are fp32 only: int8 batches run multi-launch
     d->pok = false;
+    d->pk = false;
+    (void)hipFree(d->pkgran);
+    d->pkgran = nullptr;
     d->pwhy = "int8 weights with batch > 1";
   }
   // persistent step with int8 weights: re-check the shape (group size, LDS) and publish the

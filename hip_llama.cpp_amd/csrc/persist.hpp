@@ -50,6 +50,8 @@ struct PStep {
   int B;                    // batched step (persist_b.hip): 2..8 sequences; tok / pos / out and every
                             // hand-off buffer then hold B rows, bmax [grid][8], tickets [L][B*H];
                             // n_scr = the LDS row-chunk partials (persistent_prepare_b)
+  unsigned long long* gk;   // K-split step (persist_k.hip): its hand-off area, persistent_k_granules
+                            // granules, zeroed once at allocation
 };
 
 constexpr int kPSyncWords = 8 * 32;   // 8 shard counters, one 128-B line each
@@ -70,5 +72,10 @@ inline bool persistent_long_ctx(int pos) { return pos + 1 >= kAttnHelpMinKeys; }
 // The same for 2..8 sequences with fp32 weights (persist_b.hip; p.B set).
 bool persistent_prepare_b(PStep& p, int ncu, const char** why);
 hipError_t launch_persistent_step_b(const PStep& p, hipStream_t s, int ncu);
+// 8 sequences with fp32 weights, every GEMV phase K-split over the CUs (persist_k.hip): the
+// granules its hand-off area needs (PStep::gk), the shape check, the launch.
+long long persistent_k_granules(const PStep& p, int ncu);
+bool persistent_prepare_k(PStep& p, int ncu, const char** why);
+hipError_t launch_persistent_step_k(const PStep& p, hipStream_t s, int ncu);
 
 }  // namespace tl

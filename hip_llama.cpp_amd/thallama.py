@@ -92,6 +92,7 @@ STATUS = {0: "SUCCESS", 1: "NOT_INITIALIZED", 2: "ALLOC_FAILED", 3: "INVALID_VAL
 K_QKV, K_ATTN, K_WO, K_FFN_UP, K_FFN_DOWN, K_CLS, K_ARGMAX, K_STEP = range(8)
 K_NAMES = ["qkv", "attn", "wo", "ffn_up", "ffn_down", "cls", "argmax", "step"]
 OPT_NT_WEIGHTS, OPT_ATTN_SPLITS, OPT_USE_GRAPH, OPT_PROFILE, OPT_PERSISTENT, OPT_PERSIST_FAULT = 1, 2, 3, 4, 5, 6
+OPT_KSPLIT = 7
 
 _lib = None
 
@@ -154,6 +155,7 @@ def lib():
             "thallama_decoder_destroy": (None, [VP]),
             "thallama_decoder_set": (I, [VP, I, I]),
             "thallama_decoder_persistent": (I, [VP]),
+            "thallama_decoder_ksplit": (I, [VP]),
             "thallama_persistent_cooperative": (I, []),
             "thallama_decoder_granules": (I, [VP, C.POINTER(C.c_ulonglong), S]),
             "thallama_decoder_prefill": (I, [VP, I, c_int_p, I, I]),
@@ -433,6 +435,10 @@ class Decoder:
     def persistent(self):
         """True if steps run as one persistent launch (persist.hip)."""
         return bool(lib().thallama_decoder_persistent(self.h))
+
+    def ksplit(self):
+        """True if the persistent step is the K-split one (8 sequences, csrc/persist_k.hip)."""
+        return bool(lib().thallama_decoder_ksplit(self.h))
 
     def ptrace(self, enable=True):
         """Enable the persistent-step timeline; returns the stamps of the last launch as a

@@ -1,0 +1,139 @@
+"""GPU parity of the K-split persistent decode step (hip_llama.cpp_amd/csrc/persist_k.hip: the whole
+step of 8 sequences as ONE launch, every GEMV phase owned by (row group, K slice) tiles, fp32)
+against the CPU oracle (the reference's src/seq.cpp forward, pinned in tests/test_oracle.py).
+
+Bar (BASELINE.json north_star): every sequence's greedy tokens equal its own CPU decode's; fp32
+logits within 1e-4 under the reference's abs-or-rel rule (scripts/test/thaDNN.test.cpp:224-229).
+The step sums each row's 8 K-slice partials in a fixed order and applies RMSNorm as (W (w * x)) * ss
+(persist_b.hip's form), last-bit differences from src/seq.cpp the same rule covers; the fixed order
+makes it deterministic (bitwise-equal logits on a repeated step).
+Shapes: the two instantiated K-slice classes — llama2-7B's dim 4096 / hidden 11008 (slices of 2 and
+5.4 wave-loads: the 8-, 16- and 32-value wave reductions) at 2 layers, and dim 2048 / hidden 5632
+(1 and 2.75 wave-loads) with head 128 and head 64 + GQA.
+"""
+import numpy as np
+import pytest
+
+from helpers import assert_ref_close
+
+pytestmark = pytest.mark.gpu
+
+B = 8
+K2048 = (2048, 5632, 2, 16, 16, 1024, 256)        # head 128
+K2048_GQA = (2048, 5632, 2, 32, 8, 1024, 256)     # head 64, kv_dim 512
+K7B2 = (4096, 11008, 2, 32, 32, 1024, 256)        # llama2-7B layer shape, 2 layers
+
+
+def decoder(tl, cfg, seed, persistent=1, ksplit=1):
+    c = tl.Config.make(*cfg)
+    model = tl.DeviceModel(c, 0, seed=seed)
+    state = tl.DeviceState(c, B)
+    dec = tl.Decoder(model, state)
+    dec.set(tl.OPT_PERSISTENT, persistent)
+    dec.set(tl.OPT_KSPLIT, ksplit)
+    return (model, state), dec
+
+
+@pytest.mark.parametrize("cfg", [K2048, K2048_GQA, K7B2])
+def test_selected_by_default(gpu, cfg):
+    c = gpu.Config.make(*cfg)
+    model = gpu.DeviceModel(c, 0, seed=1)
+    state = gpu.DeviceState(c, B)
+    dec = gpu.Decoder(model, state)
+    assert dec.persistent() and dec.ksplit()
+
+
+@pytest.mark.parametrize("cfg", [K2048, K2048_GQA, K7B2])
+def test_independent_positions_match_oracle(gpu, oracle, cfg):
+    """8 sequences at different positions, teacher-forced random tokens: every sequence's logits
+    within 1e-4 of its own CPU decode at every step."""
+    keep, dec = decoder(gpu, cfg, 5)
+    assert dec.ksplit()
+    rng = np.random.default_rng(3)
+    starts = rng.integers(0, 12, B)
+    toks = rng.integers(0, cfg[5], (B, 40))
+    refs = [oracle.Model(cfg, 0, seed=5) for _ in range(B)]
+    for b in range(B):
+        for p in range(int(starts[b])):
+            refs[b].forward(int(toks[b, p]), p)
+    for p in range(int(starts.max())):
+        dec.forward([int(toks[b, p]) for b in range(B)], [p] * B, want_logits=False)
+    for step in range(6 if cfg is K7B2 else 10):
+        ps = [int(starts[b]) + step for b in range(B)]
+        tk = [int(toks[b, ps[b]]) for b in range(B)]
+        got = dec.forward(tk, ps)
+        for b in range(B):
+            assert_ref_close(got[b], refs[b].forward(tk[b], ps[b]), 1e-4, f"b={b} pos={ps[b]}")
+    assert dec.ksplit()  # no wait gave up
+
+
+@pytest.mark.parametrize("cfg", [K2048, K2048_GQA])
+@pytest.mark.parametrize("graph", [0, 1])
+def test_greedy_matches_oracle(gpu, oracle, cfg, graph):
+    """Greedy decode of 8 sequences from different start tokens, argmax in the step's tail: every
+    sequence's tokens equal the oracle's greedy decode."""
+    keep, dec = decoder(gpu, cfg, 42)
+    dec.set(gpu.OPT_USE_GRAPH, graph)
+    starts = [1 + 37 * b for b in range(B)]
+    n = 32
+    got = dec.greedy(starts, [0] * B, n)
+    assert dec.ksplit()
+    for b in range(B):
+        want = oracle.Model(cfg, 0, seed=42).greedy(starts[b], 0, n)
+        assert got[:, b].tolist() == want, f"sequence {b}"
+
+
+def test_long_context(gpu, oracle):
+    """Past many 16-key attention chunks (the units split each head's keys NS ways)."""
+    cfg = K2048_GQA
+    keep, dec = decoder(gpu, cfg, 21)
+    refs = [oracle.Model(cfg, 0, seed=21) for _ in range(B)]
+    toks = np.random.default_rng(8).integers(0, cfg[5], (B, 240))
+    for p in range(240):
+        want = [refs[b].forward(int(toks[b, p]), p) for b in range(B)]
+        got = dec.forward(toks[:, p].tolist(), [p] * B, want_logits=(p % 47 == 0 or p == 239))
+        if got is not None:
+            for b in range(B):
+                assert_ref_close(got[b], want[b], 1e-4, f"b={b} pos={p}")
+    assert dec.ksplit()
+
+
+def test_repeated_step_bitwise(gpu):
+    """The same step (same K/V cache, tokens, positions) twice in one process: bitwise-identical
+    logits (fixed-order K-group sums and norms; no atomics in the arithmetic)."""
+    keep, dec = decoder(gpu, K7B2, 9)
+    toks = [3 + 101 * b for b in range(B)]
+    for p in range(5):
+        dec.forward(toks, [p] * B, want_logits=False)
+    a = dec.forward(toks, [5] * B)
+    b = dec.forward(toks, [5] * B)
+    assert np.array_equal(a, b)
+
+
+def test_matches_multilaunch_tokens(gpu):
+    """Same greedy tokens as the multi-launch batched step on the 7B layer shape."""
+    keep, dk = decoder(gpu, K7B2, 7, 1)
+    keep2, dm = decoder(gpu, K7B2, 7, 0)
+    assert dk.ksplit() and not dm.persistent()
+    starts = [1 + 100 * b for b in range(B)]
+    a = dk.greedy(starts, [0] * B, 48)
+    m = dm.greedy(starts, [0] * B, 48)
+    assert (a == m).all()
+
+
+@pytest.mark.parametrize("graph", [0, 1])
+def test_give_up_falls_back(gpu, oracle, graph):
+    """A K-split launch missing a block gives up (bounded waits), the path is disabled and the
+    call re-runs on the multi-launch step: tokens still the oracle's."""
+    cfg = K2048
+    keep, dec = decoder(gpu, cfg, 42)
+    dec.set(gpu.OPT_USE_GRAPH, graph)
+    starts = [1, 5, 9, 200, 300, 400, 500, 600]
+    want = [oracle.Model(cfg, 0, seed=42).greedy(s, 0, 12) for s in starts]
+    got = dec.greedy(starts, [0] * B, 4)
+    assert [got[:, b].tolist() for b in range(B)] == [w[:4] for w in want]
+    assert dec.ksplit()
+    dec.set(gpu.OPT_PERSIST_FAULT, 1)
+    got = dec.greedy([w[3] for w in want], [4] * B, 8)
+    assert [got[:, b].tolist() for b in range(B)] == [w[4:12] for w in want]
+    assert not dec.persistent()

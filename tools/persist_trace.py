@@ -23,6 +23,40 @@ MODELS = {"7b": (4096, 11008, 32, 32, 32, 32000, 2048), "110m": (768, 2048, 12, 
 KINDS = ["qkv", "attn", "wo", "ffn_up", "ffn_down"]
 
 
+def ksplit_report(t, nph, G, wbytes, args):
+    """Per phase kind (medians over blocks, then over layers; us): staging (start -> slice staged),
+    first slot (staged -> streaming wave 1's first slot consumed), sweep (staged -> wave 1's last
+    slot), sweep barrier (staged -> every streaming wave done), reduce (barrier -> reduce done), the
+    phase (start -> the next phase's start, median block) and the weight rate it implies."""
+    print(f"ksplit B=8: {G} blocks, step {t[:, -1, 5].max() - t[:, 0, 0].min():.1f} us")
+    print(f"{'kind':9s}{'phase':>8s}{'stage':>8s}{'slot0':>8s}{'sweep':>8s}{'swbar':>8s}{'prep':>8s}{'reduce':>8s}{'GB/s':>8s}")
+    out = {}
+    for kind, k in (("qkv", 0), ("attn", 1), ("wo", 2), ("ffn_up", 3), ("ffn_down", 4), ("cls", nph - 1)):
+        phs = [k] if kind == "cls" else list(range(k, nph - 1, 5))
+        med = lambda a, b: float(np.median([np.median(t[:, ph, a] - t[:, ph, b]) for ph in phs]))  # noqa: E731
+        if kind == "cls":
+            phase = float(np.median(t[:, -1, 5] - t[:, -1, 0]))
+        else:
+            phase = float(np.median([np.median(t[:, ph + 1, 0] - t[:, ph, 0]) for ph in phs]))
+        if kind == "attn":
+            print(f"{kind:9s}{phase:8.2f}   units done {med(3, 0):.2f}")
+            out[kind] = {"phase": phase, "units_done": med(3, 0)}
+            continue
+        row = {"phase": phase, "stage": med(1, 0), "slot0": med(6, 1), "sweep": med(3, 1), "sweep_barrier": med(4, 1),
+               "prep": med(2, 1), "reduce": med(5, 4)}
+        row["GBps"] = wbytes[kind] / (phase * 1e-6) / 1e9
+        print(f"{kind:9s}" + "".join(f"{row[x]:8.2f}" for x in ("phase", "stage", "slot0", "sweep", "sweep_barrier", "prep", "reduce"))
+              + f"{row['GBps']:8.0f}")
+        out[kind] = row
+    # spread of the sweep over blocks (the reduce waits for the row group's slowest K slice)
+    for kind, k in (("qkv", 0), ("ffn_up", 3), ("ffn_down", 4)):
+        sw = np.mean([t[:, ph, 3] - t[:, ph, 1] for ph in range(k, nph - 1, 5)], axis=0)
+        print(f"{kind:9s} sweep per block: min {sw.min():.2f} med {np.median(sw):.2f} max {sw.max():.2f}")
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump(out, f, indent=1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="7b", choices=sorted(MODELS))
@@ -60,6 +94,9 @@ def main():
     esz = 4 if args.dtype == "f32" else 1 + 4 / 64  # int8 + one fp32 scale per 64
     wbytes = {k: v * esz for k, v in {"qkv": dim * (dim + 2 * kvd), "attn": 0, "wo": dim * dim, "ffn_up": 2 * dim * hid,
                                        "ffn_down": dim * hid, "cls": dim * V}.items()}
+    if B == 8 and dec.ksplit():  # the K-split step (persist_k.hip): its own slots, see TRACE_K there
+        ksplit_report(t, nph, G, wbytes, args)
+        return
     if B > 1:  # the batched step (persist_b.hip): its own slots, see TRACE_B there
         print(f"{args.model} B={B}: {G} blocks, step {t[:, -1, 3].max() - t[:, 0, 0].min():.1f} us")
         print(f"{'kind':9s}{'phase':>8s}{'stage0':>8s}{'slot0':>8s}{'passes':>40s}{'epi':>7s}{'GB/s':>8s}")
