@@ -188,7 +188,7 @@ struct thallama_decoder {
   long long pq8ls[7] = {};                // and the byte stride between layers
   bool pok = false;             // shape supported
   bool pk = false;              // 8 sequences: the K-split persistent step is supported (persist_k.hip)
-  bool ksplit = true;           //   and requested (THALLAMA_OPT_KSPLIT)
+  bool ksplit = true;           //   and taken when the step is persistent (THALLAMA_OPT_KSPLIT)
   unsigned long long* pkgran = nullptr;  // its hand-off area
   unsigned long long* ptrace = nullptr;  // optional timeline of the persistent step
   size_t ptrace_n = 0;
@@ -374,15 +374,18 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
     } else if (batch <= 8) {
       d->pok = tl::persistent_prepare_b(ps, d->ncu, &why);
       d->persist = batch <= kBatchPersistDefaultMax;
-      if (batch == 8) {  // the K-split step (persist_k.hip): the default at 8 sequences
+      if (batch == 8) {
+        // the K-split step (persist_k.hip) is the persistent step at 8 sequences where its shape is
+        // instantiated, but not the default: 7B fp32 1374-1376 vs 1438 tok/s multi-launch (positions
+        // 0..255), 974-976 vs 1007 at 1792..2047, same box; THALLAMA_KSPLIT=1
+        // in the environment selects it at creation (THALLAMA_OPT_PERSISTENT per decoder)
         tl::PStep pk = ps;
         const char* kwhy = nullptr;
         d->pk = tl::persistent_prepare_k(pk, d->ncu, &kwhy);
-        const char* ev = getenv("THALLAMA_KSPLIT");
-        d->ksplit = !(ev && ev[0] == '0');
         if (d->pk) {
           d->pok = true;
-          d->persist = d->ksplit;
+          const char* ev = getenv("THALLAMA_KSPLIT");
+          d->persist = ev && ev[0] == '1';
         }
       }
     } else {

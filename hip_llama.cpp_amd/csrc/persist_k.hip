@@ -56,15 +56,24 @@ constexpr int PW = 8;           // waves per block: 1 control + 7 streaming (two
 constexpr int PT = PW * 64;
 constexpr int NSW = PW - 1;
 constexpr int NBUF = 2;         // register slots in flight per streaming wave
-constexpr int NBL = 0;          // and LDS slots (LDS-DMA: bytes in flight without registers; a third
+#ifndef PK_NBL
+#define PK_NBL 0
+#endif
+constexpr int NBL = PK_NBL;          // and LDS slots (LDS-DMA: bytes in flight without registers; a third
                                 // register slot spilled)
 constexpr int NBT = NBUF + NBL; // slots in flight per streaming wave
 constexpr int PLM = 8;          // wave-loads (1 KiB) per slot at most
 constexpr int SBU = 4;          // staging: (sequence, float4) units in flight per thread
 constexpr int kRes = 64;        // residual rows per block and sequence (a sub-slice of dim)
 constexpr int kRcs = 64;        // QKV items per reduce sub-slice (RoPE table in LDS)
-constexpr int kMaxSlots = 1024; // slots per phase and block at most (rows of a row group)
+constexpr int kMaxSlots = 1280; // slots per phase and block at most (rows of a row group)
 constexpr unsigned kSpinLimit = 1u << 18;
+// Re-poll pause of the hand-off waits on the critical path (staging, reduce, attention inputs):
+// common.hpp gran_backoff's long form (up to 2048 cycles after 6 misses).
+#ifndef PK_POLL_LONG
+#define PK_POLL_LONG 1
+#endif
+constexpr bool kPollLong = PK_POLL_LONG;  // (short pauses: 1308 vs 1394-1418 tok/s, the extra polls slow the sweeps)
 
 enum PKind : int { PK_QKV = 0, PK_ATTN = 1, PK_WO = 2, PK_UP = 3, PK_DOWN = 4, PK_CLS = 5 };
 
@@ -162,15 +171,31 @@ struct KGeo {
   int k4lo, n4;      // the K slice (float4 units)
   int ssi;           // the sub-slice's index among all G (sums of squares, in row order)
 };
+// Row groups get items in proportion to their XCD's streaming rate: the row groups of the even
+// XCDs (rg / (G / 64) even) kXcdSkew percent more than the odd ones, which stream that much
+// slower (ffn_up 49.6-50.9 vs 53.5-55.3 us per block, qkv and ffn_down likewise:
+// tools/persist_trace.py --batch 8).  rg_weight(r) = the weight of row groups 0..r-1.
+#ifndef PK_XCD_SKEW
+#define PK_XCD_SKEW 0
+#endif
+constexpr unsigned kXcdSkew = PK_XCD_SKEW;  // (7 balanced the per-XCD sweeps but not the step: measured, round 6)
+__host__ __device__ inline long long rg_weight(int r, int G) {
+  const int per = G >> 6;  // row groups per XCD
+  const int x = r / per, rem = r - x * per;
+  // whole XCDs before r: pairs (even, odd) weigh 200 + skew per row group
+  const long long full = (long long)(x >> 1) * per * (200 + kXcdSkew) + (x & 1) * (long long)per * (100 + kXcdSkew);
+  return full + (long long)rem * ((x & 1) ? 100 : 100 + kXcdSkew);
+}
+
 TL_DEVICE KGeo geo(const KDesc& d) {
   KGeo g;
   const int G = gridDim.x, bi = blockIdx.x;
   const int j = bi >> 3;
   g.kg = j & 7;
   g.rg = (bi & 7) * (G >> 6) + (j >> 3);
-  const long long NRG = G >> 3, n = d.n_items;
-  g.i0 = (int)(n * g.rg / NRG);
-  g.ni = (int)(n * (g.rg + 1) / NRG) - g.i0;
+  const long long n = d.n_items;
+  g.i0 = (int)(n * rg_weight(g.rg, G) / rg_weight(G >> 3, G));
+  g.ni = (int)(n * rg_weight(g.rg + 1, G) / rg_weight(G >> 3, G)) - g.i0;
   g.nrow = g.ni * d.rpi;
   g.s0 = g.i0 + g.ni * g.kg / NKG;
   g.ns = g.i0 + g.ni * (g.kg + 1) / NKG - g.s0;
@@ -397,7 +422,7 @@ TL_DEVICE void stage(const KDesc& d, const KGeo& g, const PStep& p, f4* xs) {
         const int k4 = g.k4lo + j;
         if (d.gin)
           v = gran4_ok(ga[k], gb[k], d.tag_in) ? gran4_val(ga[k], gb[k])
-                                               : gran_wait4(r, (unsigned)(b * K4 + k4) * 32u, d.tag_in, p.err, true);
+                                               : gran_wait4(r, (unsigned)(b * K4 + k4) * 32u, d.tag_in, p.err, kPollLong);
         else
           v = reinterpret_cast<const f4*>(p.emb + (long long)p.tok[b] * p.dim)[k4];
         if (d.rms) {
@@ -501,7 +526,7 @@ TL_DEVICE void reduce(const KDesc& d, const KGeo& g, const PStep& p, int l, floa
       for (int kg = 0; kg < NKG; ++kg) {
         const float e = (unsigned)(x[r][kg] >> 32) == d.tag_out || (r == 1 && !two)
                             ? __uint_as_float((unsigned)x[r][kg])
-                            : gran_wait(src + kg * rows * NB + r * NB, d.tag_out, p.err, true);
+                            : gran_wait(src + kg * rows * NB + r * NB, d.tag_out, p.err, kPollLong);
         s = kg == 0 ? e : __fadd_rn(s, e);
       }
       v[r] = d.rms ? __fmul_rn(s, sscale[b]) : s;
@@ -643,7 +668,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, f4* xs, f4* rings, flo
         aw.gout = p.gk + k.act0 + (l & 1) * k.act + k.xb;
         aw.etab = etab;
         aw.tag_in = tb + 5u * l + 1; aw.tag_out = tb + 5u * l + 2; aw.err = p.err;
-        aw.poll_long = 1;
+        aw.poll_long = kPollLong;
         const int units = NB * p.H * p.NS;
         for (int u = blockIdx.x + G * wave; u < units; u += G * PW) attn_unit<HS, 16, true>(aw, u, lane);
         if constexpr (ROLE0) TRACE_K(3);
@@ -784,7 +809,7 @@ static long long max_group_rows(const PStep& p, int ncu) {
   const long long nrg = ncu / NKG;
   long long m = 0;
   for (long long n : {2ll * ((p.dim + 2ll * p.kvd) / 2), (long long)p.dim, 2ll * p.hid, (long long)p.V}) {
-    const long long r = (n + nrg - 1) / nrg + 2;
+    const long long r = (n * (100 + kXcdSkew) * nrg / rg_weight((int)nrg, ncu) + nrg - 1) / nrg + 2;
     m = r > m ? r : m;
   }
   return m;
@@ -815,7 +840,9 @@ bool persistent_prepare_k(PStep& p, int ncu, const char** why) {
   if (p.NS < 1 || p.NS > kMaxNS) return fail("attention splits out of range");
   if (5 * p.L + 2 >= 4096) return fail("too many layers for the phase tags");
   const int nrg = ncu / NKG;
-  auto sub = [&](long long n) { return (n + nrg - 1) / nrg / NKG + 2; };  // items per reduce sub-slice, at most
+  auto sub = [&](long long n) {  // items per reduce sub-slice, at most (the even XCDs' row groups)
+    return n * (100 + kXcdSkew) / rg_weight(nrg, ncu) / NKG + 2;
+  };
   if (sub(p.dim) > kRes) return fail("residual rows per block exceed the LDS slice");
   if (sub((p.dim + 2 * p.kvd) / 2) > kRcs) return fail("QKV items per block exceed the RoPE table");
   if ((long long)NB * (p.dim + 2 * p.kvd) * 8 >= (1ll << 31)) return fail("granule offsets exceed 31 bits");

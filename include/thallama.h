@@ -34,16 +34,18 @@ enum {
   THALLAMA_OPT_PROFILE = 4,      /* 0/1: HIP events around every kernel class (eager only) */
   THALLAMA_OPT_PERSISTENT = 5,   /* 0/1: whole step as ONE persistent launch (fp32 batch 1..8,
                                     int8 batch 1; head size 64/128).  Default 1 where supported,
-                                    except fp32 batch 5..7 (default 0: slower than multi-launch
-                                    there; batch 8 runs the K-split step).  Profiled as the single class THALLAMA_K_STEP. */
+                                    except fp32 batch 5..8 (default 0: slower than multi-launch
+                                    there; at batch 8 it is the K-split step).  Profiled as the single class THALLAMA_K_STEP. */
   THALLAMA_OPT_PERSIST_FAULT = 6,  /* test hook: the next persistent launch runs without its
                                     block 0 (as if the grid were not co-resident): its waits
                                     give up, the call disables the path and re-runs on the
                                     multi-launch step. */
   THALLAMA_OPT_KSPLIT = 7,       /* 0/1: at 8 sequences the persistent step gives each CU a
                                     (row group, K slice) tile (persist_k.hip) instead of whole
-                                    rows (persist_b.hip).  Default 1 where the shape is supported;
-                                    THALLAMA_KSPLIT=0 in the environment at creation sets 0. */
+                                    rows (persist_b.hip).  Default 1 where the shape is supported
+                                    (the persistent step itself stays off by default at 8
+                                    sequences; THALLAMA_KSPLIT=1 in the environment at creation,
+                                    or THALLAMA_OPT_PERSISTENT=1, turns it on). */
 };
 
 /* 1 if the decoder runs its steps as one persistent launch (THALLAMA_OPT_PERSISTENT

@@ -34,12 +34,19 @@ def decoder(tl, cfg, seed, persistent=1, ksplit=1):
     return (model, state), dec
 
 
-@pytest.mark.parametrize("cfg", [K2048, K2048_GQA, K7B2])
-def test_selected_by_default(gpu, cfg):
+K7B_V = (4096, 11008, 1, 32, 32, 32000, 256)     # one llama2-7B layer + its 32000-row classifier
+
+
+@pytest.mark.parametrize("cfg", [K2048, K2048_GQA, K7B2, K7B_V])
+def test_selected_when_persistent(gpu, cfg):
+    """The instantiated shapes (the 7B one with its 32000-row classifier too) prepare the K-split
+    step; it is opt-in (the multi-launch step stays the default at 8 sequences: DESIGN.md section 7)."""
     c = gpu.Config.make(*cfg)
     model = gpu.DeviceModel(c, 0, seed=1)
     state = gpu.DeviceState(c, B)
     dec = gpu.Decoder(model, state)
+    assert not dec.persistent() and not dec.ksplit()
+    dec.set(gpu.OPT_PERSISTENT, 1)
     assert dec.persistent() and dec.ksplit()
 
 

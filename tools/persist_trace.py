@@ -49,9 +49,14 @@ def ksplit_report(t, nph, G, wbytes, args):
               + f"{row['GBps']:8.0f}")
         out[kind] = row
     # spread of the sweep over blocks (the reduce waits for the row group's slowest K slice)
-    for kind, k in (("qkv", 0), ("ffn_up", 3), ("ffn_down", 4)):
+    bi = np.arange(G)
+    kg = (bi >> 3) & 7
+    for kind, k in (("qkv", 0), ("wo", 2), ("ffn_up", 3), ("ffn_down", 4)):
         sw = np.mean([t[:, ph, 3] - t[:, ph, 1] for ph in range(k, nph - 1, 5)], axis=0)
-        print(f"{kind:9s} sweep per block: min {sw.min():.2f} med {np.median(sw):.2f} max {sw.max():.2f}")
+        print(f"{kind:9s} sweep per block: min {sw.min():.2f} med {np.median(sw):.2f} max {sw.max():.2f}; by XCD "
+              + " ".join(f"{sw[bi % 8 == x].mean():.1f}" for x in range(8)) + "; by K group "
+              + " ".join(f"{sw[kg == x].mean():.1f}" for x in range(8)))
+        out[kind + "_sweep_by_xcd"] = [float(sw[bi % 8 == x].mean()) for x in range(8)]
     if args.json:
         with open(args.json, "w") as f:
             json.dump(out, f, indent=1)
@@ -76,6 +81,8 @@ def main():
     B = args.batch
     state = tl.DeviceState(c, B)
     dec = tl.Decoder(model, state)
+    if B > 1:
+        dec.set(tl.OPT_PERSISTENT, 1)  # (opt-in at 5..8 sequences; at 8 the K-split step)
     assert dec.persistent()
     dec.greedy([1] * B, [0] * B, args.pos, want_tokens=False)
     dec.ptrace(True)
