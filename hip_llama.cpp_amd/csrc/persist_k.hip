@@ -62,6 +62,24 @@ constexpr int NBUF = 2;         // register slots in flight per streaming wave
 constexpr int NBL = PK_NBL;          // and LDS slots (LDS-DMA: bytes in flight without registers; a third
                                 // register slot spilled)
 constexpr int NBT = NBUF + NBL; // slots in flight per streaming wave
+// The next phase's slots a streaming wave issues before that phase's input is staged, and when:
+// ONE slot, after this phase's reduce.  Weight loads in flight slow the latency-bound hand-off loads
+// they share the memory path with (7B B=8, same box: two slots after the sweep 1226 tok/s, one
+// slot after the sweep 1399, two after the reduce 1256, one after the reduce 1425, none 1349 on
+// another box where two after the sweep gave 1363 and one 1379; profiles/r06/ksplit_ab.txt).
+#ifndef PK_PREFETCH_SLOTS
+#define PK_PREFETCH_SLOTS 1
+#endif
+constexpr int kPrefetchSlots = PK_PREFETCH_SLOTS;
+#ifndef PK_PREFETCH_AFTER_REDUCE
+#define PK_PREFETCH_AFTER_REDUCE 1
+#endif
+constexpr bool kPrefetchAfterReduce = PK_PREFETCH_AFTER_REDUCE;
+#ifndef PK_PREFETCH_WAVES
+#define PK_PREFETCH_WAVES NSW
+#endif
+constexpr int kPrefetchWaves = PK_PREFETCH_WAVES;  // streaming waves that prefetch (the first ones)
+
 constexpr int PLM = 8;          // wave-loads (1 KiB) per slot at most
 constexpr int SBU = 4;          // staging: (sequence, float4) units in flight per thread
 constexpr int kRes = 64;        // residual rows per block and sequence (a sub-slice of dim)
@@ -355,6 +373,7 @@ template <int RW>
 TL_DEVICE void prefetch(const KDesc& d, const KGeo& g, const PStep& p, int sw, int lane, f4 (&buf)[NBUF][PLM], f4* ring) {
 #pragma unroll
   for (int i = 0; i < NBT; ++i) {
+    if (i >= kPrefetchSlots || sw >= kPrefetchWaves) continue;  // (the rest: loaded when the sweep starts)
     if (i < NBUF) load_slot<RW>(d, g, p, sw + i * NSW, lane, buf[i < NBUF ? i : 0]);
     else load_slot_lds<RW>(d, g, p, sw + i * NSW, lane, ring + (i - NBUF) * PLM * 64);
   }
@@ -370,6 +389,12 @@ TL_DEVICE void run_slots(const KDesc& d, const KGeo& g, const PStep& p, int sw, 
   int sl[NBT];
 #pragma unroll
   for (int i = 0; i < NBT; ++i) sl[i] = sw + i * NSW;
+#pragma unroll
+  for (int i = 0; i < NBT; ++i) {  // the initial slots prefetch() did not issue
+    if (i < kPrefetchSlots && sw < kPrefetchWaves) continue;
+    if (i < NBUF) load_slot<RW>(d, g, p, sl[i], lane, buf[i < NBUF ? i : 0]);
+    else load_slot_lds<RW>(d, g, p, sl[i], lane, ring + (i - NBUF) * PLM * 64);
+  }
   while (sl[0] < nslot) {  // (sl[0] < sl[1] < ... always: a later take draws a larger slot)
 #pragma unroll
     for (int i = 0; i < NBT; ++i) {
@@ -605,6 +630,21 @@ TL_DEVICE void grid_barrier(const PStep& p) {
   __syncthreads();
 }
 
+// The next GEMV phase's first slots after phase `kind` of layer l (none after QKV: the attention
+// units run first, and the streaming waves issue Wo's after theirs; none after the classifier).
+template <int RWD, int RWH>
+TL_DEVICE void prefetch_next(const PStep& p, int kind, int l, unsigned tb, int sw, int lane, f4 (&buf)[NBUF][PLM],
+                             f4* ring) {
+  if (kind == PK_WO || kind == PK_UP) {
+    const KDesc nd = make_desc(p, kind + 1, l, tb);
+    if (kind + 1 == PK_DOWN) prefetch<RWH>(nd, geo(nd), p, sw, lane, buf, ring);
+    else prefetch<RWD>(nd, geo(nd), p, sw, lane, buf, ring);
+  } else if (kind == PK_DOWN) {
+    const KDesc nd = l + 1 < p.L ? make_desc(p, PK_QKV, l + 1, tb) : make_desc(p, PK_CLS, p.L, tb);
+    prefetch<RWD>(nd, geo(nd), p, sw, lane, buf, ring);
+  }
+}
+
 // Optional timeline (PStep::trace, [grid][5L+1][kTraceSlots], 100-MHz clock; tools/persist_trace.py
 // --batch 8): control wave — 0 phase start, 1 slice staged, 2 norm scales / RoPE ready, 4 sweep
 // barrier passed, 5 reduce done (attention: 3 units done); streaming wave 1 — 6 first slot
@@ -697,14 +737,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, f4* xs, f4* rings, flo
       if (ts && lane == 0) ts[3] = __builtin_amdgcn_s_memrealtime();
       // the next GEMV phase's first slots: in flight through both hand-offs and its staging
       // (after QKV: once the attention units ran)
-      if (kind == PK_WO || kind == PK_UP) {
-        const KDesc nd = make_desc(p, kind + 1, l, tb);
-        if (kind + 1 == PK_DOWN) prefetch<RWH>(nd, geo(nd), p, sw, lane, buf, ring);
-        else prefetch<RWD>(nd, geo(nd), p, sw, lane, buf, ring);
-      } else if (kind == PK_DOWN) {
-        const KDesc nd = l + 1 < p.L ? make_desc(p, PK_QKV, l + 1, tb) : make_desc(p, PK_CLS, p.L, tb);
-        prefetch<RWD>(nd, geo(nd), p, sw, lane, buf, ring);
-      }
+      if (!kPrefetchAfterReduce) prefetch_next<RWD, RWH>(p, kind, l, tb, sw, lane, buf, ring);
     }
     __syncthreads();  // the block's partials published; norm scales / RoPE table in LDS
     if constexpr (ROLE0) {
@@ -712,6 +745,9 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, f4* xs, f4* rings, flo
       if (lane == 0) *ctr = 0u;  // the next phase's slot counter (used after its staging barrier)
     }
     reduce(d, g, p, l, xres, ssred, sscale, rcs, etab, cbest, wave, lane);
+    if constexpr (!ROLE0) {
+      if (kPrefetchAfterReduce) prefetch_next<RWD, RWH>(p, kind, l, tb, sw, lane, buf, ring);
+    }
     if constexpr (ROLE0) TRACE_K(5);
   }
   __syncthreads();  // every wave's classifier winners in cbest
