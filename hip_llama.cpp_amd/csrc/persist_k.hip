@@ -15,8 +15,10 @@
 //     the 8 blocks of a row group (its 8 K slices) share one XCD and one L2;
 //   * phase input (B x K floats) -> the block stages x[b][K slice kg] (K / 8 per sequence: 16 KiB
 //     of granules at K = 4096) into LDS, times the RMSNorm weight where the phase has one;
-//   * the streaming waves sweep the row group's rows over that slice and publish each row's 8
-//     partial dot products as granules P[kg][row][b] (in the slot, no LDS round trip);
+//   * the streaming waves sweep the row group's rows over that slice; each slot's row partials of
+//     the 8 sequences go to LDS, and the control wave publishes finished slots as granules
+//     P[kg][row][b] while the sweep runs (a global store in the streaming waves sat in their vmcnt
+//     queue ahead of the next slot's loads);
 //   * reduce-scatter inside the row group: block (rg, kg) owns sub-slice kg of the row group's
 //     items, sums their 8 partials in K-group order (fixed: deterministic), applies the norm scale
 //     and the fused epilogue (RoPE + K/V row, residual, SwiGLU, logits + argmax) and publishes the
@@ -25,8 +27,8 @@
 //     sum of squares): the residual phases' reducers publish per-sub-slice sums of squares and
 //     the normed phases' control waves add them up (fixed order) while the rows stream.
 // Two hand-offs per phase (partials, then outputs) of ~1-2 KiB per block each, instead of one
-// all-gather of B x K granules; the streaming waves issue the next phase's first slots before
-// both, as in the other engines.
+// all-gather of B x K granules; each streaming wave has one slot of the next phase in flight across
+// them, issued after the reduce (more weight traffic there slows the hand-offs: kPrefetchSlots).
 //
 // Hand-off buffers (granules, PStep::gk) are per kind and layer PARITY: a block writes the buffers
 // of phase (l + 2) only after its staging of that phase, which transitively waited for every
@@ -56,12 +58,8 @@ constexpr int PW = 8;           // waves per block: 1 control + 7 streaming (two
 constexpr int PT = PW * 64;
 constexpr int NSW = PW - 1;
 constexpr int NBUF = 2;         // register slots in flight per streaming wave
-#ifndef PK_NBL
-#define PK_NBL 0
-#endif
-constexpr int NBL = PK_NBL;          // and LDS slots (LDS-DMA: bytes in flight without registers; a third
-                                // register slot spilled)
-constexpr int NBT = NBUF + NBL; // slots in flight per streaming wave
+// (a third register slot spilled; a third slot in LDS by LDS-DMA, during the sweep or only across
+// the boundary, lost 2-3%: DESIGN.md section 7)
 // The next phase's slots a streaming wave issues before that phase's input is staged, and when:
 // ONE slot, after this phase's reduce.  Weight loads in flight slow the latency-bound hand-off loads
 // they share the memory path with (7B B=8, same box: two slots after the sweep 1226 tok/s, one
@@ -256,25 +254,6 @@ TL_DEVICE void load_slot(const KDesc& d, const KGeo& g, const PStep& p, int s, i
   }
 }
 
-// The same into LDS slot `ls` (PLM KiB of the wave's ring) by LDS-DMA: wave-load (r, u) lands at
-// ls[(r * RW + u) * 64 + lane] (float4).  Completion is tracked by the issuing wave's vmcnt (the
-// compiler waits for it before the consume's LDS reads).
-template <int RW>
-TL_DEVICE void load_slot_lds(const KDesc& d, const KGeo& g, const PStep& p, int s, int lane, f4* ls) {
-  constexpr int SR = sr_of(RW);
-#pragma unroll
-  for (int r = 0; r < SR; ++r) {
-    const int rl = s * SR + r;
-    const bool live = rl < g.nrow;
-    const float* row = row_ptr(d, p, g.i0 * d.rpi + (live ? rl : 0)) + 4 * g.k4lo;
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(row), (short)0, live ? g.n4 * 16 : 0, 0x00020000);
-#pragma unroll
-    for (int u = 0; u < RW; ++u)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(ls + (r * RW + u) * 64), 16,
-                                               lane * 16 + u * 1024, 0, 0, 2 /*nt*/);
-  }
-}
-
 // Consume slot s: SR rows x RW wave-loads against the staged slice (the same columns for every
 // row, so each slice read serves SR rows), then publish the SR x NB partials of the slot as granules
 // P[kg][row][b] (contiguous: rows of the slot, sequences within a row).  The slice is staged as 8
@@ -283,9 +262,9 @@ TL_DEVICE void load_slot_lds(const KDesc& d, const KGeo& g, const PStep& p, int 
 // multiplies sequence PAIRS with one packed FMA (v_pk_fma_f32, the weight broadcast): 128 instead of
 // 256 FMA instructions per slot, half of the consume's VALU time at 8 sequences.
 typedef float f2 __attribute__((ext_vector_type(2)));
-template <int RW, bool LW>
-TL_DEVICE void consume_slot(const KDesc& d, const KGeo& g, int s, int lane, const f4 (&buf)[PLM], const f4* lw,
-                            const f4* xs, float* pres) {
+template <int RW>
+TL_DEVICE void consume_slot(const KDesc& d, const KGeo& g, int s, int lane, const f4 (&buf)[PLM], const f4* xs,
+                            float* pres) {
   constexpr int SR = sr_of(RW);
   constexpr int NV = SR * NB;
   constexpr int XS4 = RW * 64;
@@ -306,7 +285,7 @@ TL_DEVICE void consume_slot(const KDesc& d, const KGeo& g, int s, int lane, cons
     for (int k = 0; k < 8; ++k) xq[k] = xc[k * XS4 + u * 64];
 #pragma unroll
     for (int r = 0; r < SR; ++r) {
-      const f4 w = LW ? lw[(r * RW + u) * 64 + lane] : buf[r * RW + u];  // (LW: the wave's LDS slot)
+      const f4 w = buf[r * RW + u];
       const float wc[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -364,52 +343,44 @@ TL_DEVICE void publish_partials(const KDesc& d, const KGeo& g, const float* pres
 TL_DEVICE int take_slot(unsigned* ctr, int lane) {
   unsigned v = 0;
   if (lane == 0) v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  return NBT * NSW + (int)__builtin_amdgcn_readlane(v, 0);
+  return NBUF * NSW + (int)__builtin_amdgcn_readlane(v, 0);
 }
 
-// A wave's first NBT slots of a phase (its prefetch: issued before the hand-offs they overlap): the
-// register slots, then the LDS ones (ring: this wave's NBL slots of PLM KiB).
+// A wave's first slots of a phase (its prefetch: issued before the hand-offs they overlap; see
+// kPrefetchSlots for how many and when).
 template <int RW>
-TL_DEVICE void prefetch(const KDesc& d, const KGeo& g, const PStep& p, int sw, int lane, f4 (&buf)[NBUF][PLM], f4* ring) {
+TL_DEVICE void prefetch(const KDesc& d, const KGeo& g, const PStep& p, int sw, int lane, f4 (&buf)[NBUF][PLM]) {
 #pragma unroll
-  for (int i = 0; i < NBT; ++i) {
-    if (i >= kPrefetchSlots || sw >= kPrefetchWaves) continue;  // (the rest: loaded when the sweep starts)
-    if (i < NBUF) load_slot<RW>(d, g, p, sw + i * NSW, lane, buf[i < NBUF ? i : 0]);
-    else load_slot_lds<RW>(d, g, p, sw + i * NSW, lane, ring + (i - NBUF) * PLM * 64);
-  }
+  for (int i = 0; i < NBUF; ++i)
+    if (i < kPrefetchSlots && sw < kPrefetchWaves) load_slot<RW>(d, g, p, sw + i * NSW, lane, buf[i]);
 }
 
-// The sweep: the prefetched slots (sw, sw + NSW, ...), then slots dealt from the block's counter,
-// each refilling the buffer it was consumed from (slots are taken in increasing order per wave).
+// The sweep: the first slots (sw, sw + NSW; those prefetch() did not issue are issued here), then
+// slots dealt from the block's counter, each refilling the buffer it was consumed from (slots are
+// taken in increasing order per wave).
 template <int RW>
 TL_DEVICE void run_slots(const KDesc& d, const KGeo& g, const PStep& p, int sw, int lane, const f4* xs,
-                         f4 (&buf)[NBUF][PLM], f4* ring, float* pres, unsigned* sdone, unsigned mark, unsigned* ctr,
+                         f4 (&buf)[NBUF][PLM], float* pres, unsigned* sdone, unsigned mark, unsigned* ctr,
                          unsigned long long* ts) {
   const int nslot = (g.nrow + sr_of(RW) - 1) / sr_of(RW);
-  int sl[NBT];
+  int sl[NBUF];
 #pragma unroll
-  for (int i = 0; i < NBT; ++i) sl[i] = sw + i * NSW;
-#pragma unroll
-  for (int i = 0; i < NBT; ++i) {  // the initial slots prefetch() did not issue
-    if (i < kPrefetchSlots && sw < kPrefetchWaves) continue;
-    if (i < NBUF) load_slot<RW>(d, g, p, sl[i], lane, buf[i < NBUF ? i : 0]);
-    else load_slot_lds<RW>(d, g, p, sl[i], lane, ring + (i - NBUF) * PLM * 64);
+  for (int i = 0; i < NBUF; ++i) {
+    sl[i] = sw + i * NSW;
+    if (!(i < kPrefetchSlots && sw < kPrefetchWaves)) load_slot<RW>(d, g, p, sl[i], lane, buf[i]);
   }
-  while (sl[0] < nslot) {  // (sl[0] < sl[1] < ... always: a later take draws a larger slot)
+  while (sl[0] < nslot) {  // (sl[0] < sl[1] always: a later take draws a larger slot)
 #pragma unroll
-    for (int i = 0; i < NBT; ++i) {
-      f4* ls = ring + (i < NBUF ? 0 : i - NBUF) * PLM * 64;
+    for (int i = 0; i < NBUF; ++i) {
       if (sl[i] < nslot) {
-        if (i < NBUF) consume_slot<RW, false>(d, g, sl[i], lane, buf[i < NBUF ? i : 0], ls, xs, pres);
-        else consume_slot<RW, true>(d, g, sl[i], lane, buf[0], ls, xs, pres);
+        consume_slot<RW>(d, g, sl[i], lane, buf[i], xs, pres);
         // the slot's partials are in pres: the control wave may publish them (release: after them)
         if (lane == 0) __hip_atomic_store(sdone + sl[i], mark, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       if (i == 0 && ts && lane == 0 && sl[0] == sw) ts[6] = __builtin_amdgcn_s_memrealtime();  // first slot in
       __builtin_amdgcn_sched_barrier(0);
       sl[i] = take_slot(ctr, lane);
-      if (i < NBUF) load_slot<RW>(d, g, p, sl[i], lane, buf[i < NBUF ? i : 0]);
-      else load_slot_lds<RW>(d, g, p, sl[i], lane, ls);
+      load_slot<RW>(d, g, p, sl[i], lane, buf[i]);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -633,15 +604,14 @@ TL_DEVICE void grid_barrier(const PStep& p) {
 // The next GEMV phase's first slots after phase `kind` of layer l (none after QKV: the attention
 // units run first, and the streaming waves issue Wo's after theirs; none after the classifier).
 template <int RWD, int RWH>
-TL_DEVICE void prefetch_next(const PStep& p, int kind, int l, unsigned tb, int sw, int lane, f4 (&buf)[NBUF][PLM],
-                             f4* ring) {
+TL_DEVICE void prefetch_next(const PStep& p, int kind, int l, unsigned tb, int sw, int lane, f4 (&buf)[NBUF][PLM]) {
   if (kind == PK_WO || kind == PK_UP) {
     const KDesc nd = make_desc(p, kind + 1, l, tb);
-    if (kind + 1 == PK_DOWN) prefetch<RWH>(nd, geo(nd), p, sw, lane, buf, ring);
-    else prefetch<RWD>(nd, geo(nd), p, sw, lane, buf, ring);
+    if (kind + 1 == PK_DOWN) prefetch<RWH>(nd, geo(nd), p, sw, lane, buf);
+    else prefetch<RWD>(nd, geo(nd), p, sw, lane, buf);
   } else if (kind == PK_DOWN) {
     const KDesc nd = l + 1 < p.L ? make_desc(p, PK_QKV, l + 1, tb) : make_desc(p, PK_CLS, p.L, tb);
-    prefetch<RWD>(nd, geo(nd), p, sw, lane, buf, ring);
+    prefetch<RWD>(nd, geo(nd), p, sw, lane, buf);
   }
 }
 
@@ -659,13 +629,12 @@ TL_DEVICE void prefetch_next(const PStep& p, int kind, int l, unsigned tb, int s
 // barriers: after the staging, and after the sweep (every partial of the block published, the
 // norm scales and RoPE table in LDS).
 template <int HS, int RWD, int RWH, bool ROLE0>
-TL_DEVICE void phases(const PStep& p, int wave, int lane, f4* xs, f4* rings, float* pres, unsigned* sdone, float* xres, float* ssred, float* sscale,
+TL_DEVICE void phases(const PStep& p, int wave, int lane, f4* xs, float* pres, unsigned* sdone, float* xres, float* ssred, float* sscale,
                       unsigned* ctr, const uint64_t* etab, float2* rcs, unsigned long long* cbest, unsigned tb) {
   const int G = gridDim.x;
   const int nph = 5 * p.L + 1;
   f4 buf[NBUF][PLM];
   const int sw = wave - 1;
-  f4* ring = rings + (sw < 0 ? 0 : sw) * (NBL * PLM * 64);  // this streaming wave's LDS slots
   if constexpr (ROLE0) {
     // this block's residual rows (its reduce sub-slice of the Wo / W2 outputs) start as the
     // embedding rows
@@ -677,7 +646,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, f4* xs, f4* rings, flo
     if (lane == 0) *ctr = 0u;
   } else {
     const KDesc d0 = make_desc(p, PK_QKV, 0, tb);
-    prefetch<RWD>(d0, geo(d0), p, sw, lane, buf, ring);
+    prefetch<RWD>(d0, geo(d0), p, sw, lane, buf);
   }
   __syncthreads();
 
@@ -715,7 +684,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, f4* xs, f4* rings, flo
       }
       if constexpr (!ROLE0) {  // Wo's first slots stream in while its input is gathered
         const KDesc nd = make_desc(p, PK_WO, l, tb);
-        prefetch<RWD>(nd, geo(nd), p, sw, lane, buf, ring);
+        prefetch<RWD>(nd, geo(nd), p, sw, lane, buf);
       }
       continue;
     }
@@ -732,12 +701,12 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, f4* xs, f4* rings, flo
       else publish_partials<RWD>(d, g, pres, sdone, (unsigned)ph + 1u, lane);
     } else {
       unsigned long long* ts = p.trace && sw == 0 ? p.trace + ((long long)blockIdx.x * nph + ph) * kTraceSlots : nullptr;
-      if (kind == PK_DOWN) run_slots<RWH>(d, g, p, sw, lane, xs, buf, ring, pres, sdone, (unsigned)ph + 1u, ctr, ts);
-      else run_slots<RWD>(d, g, p, sw, lane, xs, buf, ring, pres, sdone, (unsigned)ph + 1u, ctr, ts);
+      if (kind == PK_DOWN) run_slots<RWH>(d, g, p, sw, lane, xs, buf, pres, sdone, (unsigned)ph + 1u, ctr, ts);
+      else run_slots<RWD>(d, g, p, sw, lane, xs, buf, pres, sdone, (unsigned)ph + 1u, ctr, ts);
       if (ts && lane == 0) ts[3] = __builtin_amdgcn_s_memrealtime();
       // the next GEMV phase's first slots: in flight through both hand-offs and its staging
       // (after QKV: once the attention units ran)
-      if (!kPrefetchAfterReduce) prefetch_next<RWD, RWH>(p, kind, l, tb, sw, lane, buf, ring);
+      if (!kPrefetchAfterReduce) prefetch_next<RWD, RWH>(p, kind, l, tb, sw, lane, buf);
     }
     __syncthreads();  // the block's partials published; norm scales / RoPE table in LDS
     if constexpr (ROLE0) {
@@ -746,7 +715,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, f4* xs, f4* rings, flo
     }
     reduce(d, g, p, l, xres, ssred, sscale, rcs, etab, cbest, wave, lane);
     if constexpr (!ROLE0) {
-      if (kPrefetchAfterReduce) prefetch_next<RWD, RWH>(p, kind, l, tb, sw, lane, buf, ring);
+      if (kPrefetchAfterReduce) prefetch_next<RWD, RWH>(p, kind, l, tb, sw, lane, buf);
     }
     if constexpr (ROLE0) TRACE_K(5);
   }
@@ -796,11 +765,10 @@ __global__ void __launch_bounds__(PT) persistent_step_k_kernel(PStep p) {
   if (p.fault && blockIdx.x == 0) return;  // test hook: a missing block (every wait is bounded)
   constexpr int XSM = (RWD > RWH ? RWD : RWH) * 64;
   // dynamic LDS (kdyn_bytes): the staged K slice of every sequence (8 planes of XSM float4), then the
-  // streaming waves' LDS slots (NBL x PLM KiB each)
+  // row partials
   extern __shared__ __attribute__((aligned(16))) unsigned char kdyn[];
   f4* xs = reinterpret_cast<f4*>(kdyn);
-  f4* rings = xs + 8 * XSM;
-  float* pres = reinterpret_cast<float*>(rings + NSW * NBL * PLM * 64);  // the block's row partials [rows][NB]
+  float* pres = reinterpret_cast<float*>(xs + 8 * XSM);  // the block's row partials [rows][NB]
   __shared__ float xres[NB * kRes];                         // this block's residual rows
   __shared__ float ssred[kRes * NB];                        // their squares (sums of squares)
   __shared__ float sscale[NB];                              // the phase's norm scales
@@ -819,9 +787,9 @@ __global__ void __launch_bounds__(PT) persistent_step_k_kernel(PStep p) {
   const unsigned tb = p.seq[0] << 12;  // tag base of this launch
   if (wave == 0) {
     __builtin_amdgcn_s_setprio(2);  // the control wave's work is every other block's hand-off
-    phases<HS, RWD, RWH, true>(p, wave, lane, xs, rings, pres, sdone, xres, ssred, sscale, &ctr, etab, rcs, cbest, tb);
+    phases<HS, RWD, RWH, true>(p, wave, lane, xs, pres, sdone, xres, ssred, sscale, &ctr, etab, rcs, cbest, tb);
   } else {
-    phases<HS, RWD, RWH, false>(p, wave, lane, xs, rings, pres, sdone, xres, ssred, sscale, &ctr, etab, rcs, cbest, tb);
+    phases<HS, RWD, RWH, false>(p, wave, lane, xs, pres, sdone, xres, ssred, sscale, &ctr, etab, rcs, cbest, tb);
   }
 }
 
@@ -850,11 +818,11 @@ static long long max_group_rows(const PStep& p, int ncu) {
   }
   return m;
 }
-// Dynamic LDS of an instantiation: 8 planes of XSM float4, NSW x NBL slots of PLM KiB, the partials.
+// Dynamic LDS of an instantiation: 8 planes of XSM float4, the partials.
 static size_t kdyn_bytes(const PStep& p, int ncu) {
   const int rwd = rw_of(p.dim), rwh = rw_of(p.hid);
   const size_t xsm = (size_t)(rwd > rwh ? rwd : rwh) * 64;
-  return 8 * xsm * 16 + (size_t)NSW * NBL * PLM * 1024 + (size_t)max_group_rows(p, ncu) * NB * 4;
+  return 8 * xsm * 16 + (size_t)max_group_rows(p, ncu) * NB * 4;
 }
 
 }  // namespace pk
