@@ -187,14 +187,15 @@ struct KGeo {
   int k4lo, n4;      // the K slice (float4 units)
   int ssi;           // the sub-slice's index among all G (sums of squares, in row order)
 };
-// Row groups get items in proportion to their XCD's streaming rate: the row groups of the even
-// XCDs (rg / (G / 64) even) kXcdSkew percent more than the odd ones, which stream that much
-// slower (ffn_up 49.6-50.9 vs 53.5-55.3 us per block, qkv and ffn_down likewise:
-// tools/persist_trace.py --batch 8).  rg_weight(r) = the weight of row groups 0..r-1.
+// Row groups may get items in proportion to their XCD's streaming rate: the row groups of the even
+// XCDs (rg / (G / 64) even) kXcdSkew percent more than the odd ones, which stream that much slower
+// (ffn_up 49.6-50.9 vs 53.5-55.3 us per block, ffn_down likewise: tools/persist_trace.py --batch 8).
+// Off (0): at 7 the per-XCD sweeps evened out but the step did not move (the XCDs share one
+// bandwidth).  rg_weight(r) = the weight of row groups 0..r-1.
 #ifndef PK_XCD_SKEW
 #define PK_XCD_SKEW 0
 #endif
-constexpr unsigned kXcdSkew = PK_XCD_SKEW;  // (7 balanced the per-XCD sweeps but not the step: measured, round 6)
+constexpr unsigned kXcdSkew = PK_XCD_SKEW;
 __host__ __device__ inline long long rg_weight(int r, int G) {
   const int per = G >> 6;  // row groups per XCD
   const int x = r / per, rem = r - x * per;
@@ -255,8 +256,8 @@ TL_DEVICE void load_slot(const KDesc& d, const KGeo& g, const PStep& p, int s, i
 }
 
 // Consume slot s: SR rows x RW wave-loads against the staged slice (the same columns for every
-// row, so each slice read serves SR rows), then publish the SR x NB partials of the slot as granules
-// P[kg][row][b] (contiguous: rows of the slot, sequences within a row).  The slice is staged as 8
+// row, so each slice read serves SR rows), then the SR x NB partials of the slot, reduced over the
+// wave, into the block's LDS partials pres[row][b] (publish_partials sends them on).  The slice is staged as 8
 // planes (column c of a float4, sequences 4h..4h+3): xs[(c * 2 + h) * XS4 + j] = x[4h..4h+3][4j + c],
 // so a lane's 8 reads are contiguous across the wave (no bank conflicts) and every weight float
 // multiplies sequence PAIRS with one packed FMA (v_pk_fma_f32, the weight broadcast): 128 instead of
