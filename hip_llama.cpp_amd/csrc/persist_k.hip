@@ -135,6 +135,21 @@ struct KDesc {
   unsigned long long* gss_out;         // residual phases: this phase's sums of squares [G][NB]
 };
 
+// The attention fused into the QKV phase: row group h = head h's q, k and v rows (virtual row
+// order: head-major, q | k | v inside a head), block (h, b) reduces sequence b's rows and runs the
+// attention of (b, h) with its waves — one hand-off and the attention units' ticket combine fewer
+// per layer.  Needs one row group per head (H = G / 8), one K/V head per head and head size 128.
+// Off by default: same box, 7B B=8, 1431 vs 1416 tok/s unfused (multi-launch 1419) over positions
+// 0..255 but 770 vs 1009 at 1792..2047 — its per-wave key loop (8-B loads, one 16-key chunk in
+// flight, a wave reduction per key) is latency-bound where the attention units are not
+// (profiles/r06/ksplit_ab.txt).  Parity-tested like the rest (PK_FUSE_ATTN=1: 16 passed).
+#ifndef PK_FUSE_ATTN
+#define PK_FUSE_ATTN 0
+#endif
+TL_DEVICE bool attn_fusable(const PStep& p) {
+  return PK_FUSE_ATTN && p.H == (int)(gridDim.x >> 3) && p.kv_mul == 1 && p.hs == 128;
+}
+
 TL_DEVICE KDesc make_desc(const PStep& p, int kind, int l, unsigned tb) {
   const KLayout k = klayout(p.dim, p.hid, p.kvd, p.V, gridDim.x);
   unsigned long long* g = p.gk;
@@ -152,6 +167,7 @@ TL_DEVICE KDesc make_desc(const PStep& p, int kind, int l, unsigned tb) {
       d.gin = l == 0 ? nullptr : act(l - 1, k.xdown); d.tag_in = t0;
       d.rms = p.rms_att + ll * dim; d.gss_in = l == 0 ? nullptr : ss(l - 1, k.ssdown);
       d.gout = act(l, k.qkv); d.tag_out = t0 + 1; d.gpart = part(l, k.pqkv);
+      if (attn_fusable(p)) d.gout = act(l, k.xb);  // (its output: the attention output xb, tag t0 + 2)
       break;
     case PK_WO:
       d.K = p.dim; d.n_items = p.dim; d.rpi = 1;
@@ -196,6 +212,7 @@ struct KGeo {
 #define PK_XCD_SKEW 0
 #endif
 constexpr unsigned kXcdSkew = PK_XCD_SKEW;
+static_assert(!PK_FUSE_ATTN || PK_XCD_SKEW == 0, "the fused attention's row group h is head h: uniform row groups");
 __host__ __device__ inline long long rg_weight(int r, int G) {
   const int per = G >> 6;  // row groups per XCD
   const int x = r / per, rem = r - x * per;
@@ -223,14 +240,24 @@ TL_DEVICE KGeo geo(const KDesc& d) {
   return g;
 }
 
+// (The descriptor's matrix pointers are copied out through an empty asm first: a select between
+// struct fields became an indexed access to the struct, which then lived in scratch memory — and a
+// scratch load waits in the wave's vmcnt queue behind its weight loads.)
+TL_DEVICE const float* pick3(const KDesc& d, int i) {
+  const float *w0 = d.W0, *w1 = d.W1, *w2 = d.W2;
+  asm volatile("" : "+s"(w0), "+s"(w1), "+s"(w2));
+  return i == 0 ? w0 : i == 1 ? w1 : w2;
+}
 TL_DEVICE const float* row_ptr(const KDesc& d, const PStep& p, int R) {
   const long long K = d.K;
-  if (d.kind == PK_UP) return ((R & 1) ? d.W1 : d.W0) + (long long)(R >> 1) * K;
+  if (d.kind == PK_UP) return pick3(d, R & 1) + (long long)(R >> 1) * K;
+  if (d.kind == PK_QKV && attn_fusable(p)) {  // virtual row R = head h's row r of q | k | v
+    const int h = R / (3 * 128), r = R - h * (3 * 128);
+    return pick3(d, r >> 7) + (long long)(h * 128 + (r & 127)) * K;
+  }
   if (d.kind == PK_QKV) {
-    if (R < p.dim) return d.W0 + (long long)R * K;
-    R -= p.dim;
-    if (R < p.kvd) return d.W1 + (long long)R * K;
-    return d.W2 + (long long)(R - p.kvd) * K;
+    const int seg = R < p.dim ? 0 : R < p.dim + p.kvd ? 1 : 2;
+    return pick3(d, seg) + (long long)(R - (seg == 0 ? 0 : seg == 1 ? p.dim : p.dim + p.kvd)) * K;
   }
   return d.W0 + (long long)R * K;
 }
@@ -479,7 +506,10 @@ TL_DEVICE void prep(const KDesc& d, const KGeo& g, const PStep& p, float* sscale
       if (lane == b) sscale[b] = __fdiv_rn(1.0f, sqrtf(__fadd_rn(__fdiv_rn(tot, (float)d.K), 1e-5f)));
     }
   }
-  if (d.kind == PK_QKV) {
+  if (d.kind == PK_QKV && attn_fusable(p)) {  // the head's 64 q and 64 k pairs of sequence kg
+    for (int j = lane; j < 128; j += 64)
+      rcs[j] = p.rope[(long long)p.pos[g.kg] * (p.hs >> 1) + (j & 63)];
+  } else if (d.kind == PK_QKV) {
     for (int j = lane; j < g.ns * NB; j += 64) {
       const int it = g.s0 + j / NB, b = j % NB;
       const int row = 2 * it;
@@ -577,6 +607,128 @@ TL_DEVICE void reduce(const KDesc& d, const KGeo& g, const PStep& p, int l, floa
   }
 }
 
+// Fused QKV reduce + attention (attn_fusable), every wave of block (h, b = kg):
+//  1. sequence b's 384 rows of head h: the 8 K-group partials of each row in K-group order, the
+//     norm scale, RoPE on q and k (src/seq.cpp:86-101) -> q | k | v of (b, h) in LDS; k and v also
+//     to the K/V cache row at pos (for later steps);
+//  2. the attention of (b, h) over keys 0..T-1 (src/seq.cpp:103-136): the keys split over the
+//     block's waves, each an online softmax over 16-key chunks (cached rows from global memory,
+//     row T-1 from LDS); the waves' (max, sum, output) combined in LDS in wave order;
+//  3. the head's output published as granules (the Wo phase gathers them by K slice).
+// Differs from the reference's order only in rounding (fp32 parity, 1e-4).
+TL_DEVICE void reduce_qkv_attn(const KDesc& d, const KGeo& g, const PStep& p, int l, const float* sscale,
+                               const float2* rcs, float* lds, int wave, int lane) {
+  constexpr int HS = 128;
+  const int t = threadIdx.x, h = g.rg, b = g.kg;
+  const long long rows = (long long)d.n_items * d.rpi;
+  float* qkv = lds;  // [3 HS]
+  const int pb = p.pos[b];
+  if (t < 3 * HS / 2) {
+    const unsigned long long* src = d.gpart + ((long long)(g.i0 + t) * 2) * NB + b;
+    unsigned long long x[2][NKG];
+#pragma unroll
+    for (int kg = 0; kg < NKG; ++kg) {
+      x[0][kg] = ld8_sc1(src + kg * rows * NB);
+      x[1][kg] = ld8_sc1(src + kg * rows * NB + NB);
+    }
+    float v[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      float sum = 0.f;
+#pragma unroll
+      for (int kg = 0; kg < NKG; ++kg) {
+        const float e = (unsigned)(x[r][kg] >> 32) == d.tag_out
+                            ? __uint_as_float((unsigned)x[r][kg])
+                            : gran_wait(src + kg * rows * NB + r * NB, d.tag_out, p.err, kPollLong);
+        sum = kg == 0 ? e : __fadd_rn(sum, e);
+      }
+      v[r] = __fmul_rn(sum, sscale[b]);
+    }
+    const int seg = t / (HS / 2), c = 2 * (t % (HS / 2));  // q | k | v, column pair within the head
+    float a0 = v[0], a1 = v[1];
+    if (seg < 2) {
+      const float2 cs = rcs[t & 63];
+      const float r0 = __fsub_rn(__fmul_rn(a0, cs.x), __fmul_rn(a1, cs.y));
+      const float r1 = __fadd_rn(__fmul_rn(a0, cs.y), __fmul_rn(a1, cs.x));
+      a0 = r0; a1 = r1;
+    }
+    qkv[seg * HS + c] = a0;
+    qkv[seg * HS + c + 1] = a1;
+    if (seg > 0)  // the cache row for later steps
+      *reinterpret_cast<float2*>((seg == 1 ? p.kc : p.vc) + (long long)b * p.L * p.S * p.kvd +
+                                 ((long long)l * p.S + pb) * p.kvd + h * HS + c) = make_float2(a0, a1);
+  }
+  __syncthreads();  // q | k | v of (b, h) in LDS
+  const int T = pb + 1;
+  const int w0 = (int)((long long)T * wave / PW), w1 = (int)((long long)T * (wave + 1) / PW);
+  const float rs = sqrtf((float)HS);
+  const float2 qv = make_float2(qkv[2 * lane], qkv[2 * lane + 1]);  // lane: columns 2 lane, 2 lane + 1
+  const float* kb = p.kc + (long long)b * p.L * p.S * p.kvd + (long long)l * p.S * p.kvd + h * HS + 2 * lane;
+  const float* vb = p.vc + (long long)b * p.L * p.S * p.kvd + (long long)l * p.S * p.kvd + h * HS + 2 * lane;
+  const float2 kn = make_float2(qkv[HS + 2 * lane], qkv[HS + 2 * lane + 1]);
+  const float2 vn = make_float2(qkv[2 * HS + 2 * lane], qkv[2 * HS + 2 * lane + 1]);
+  float m = -3.402823466e+38f, lsum = 0.f;
+  float2 o = make_float2(0.f, 0.f);
+  constexpr int CH = 16;
+  for (int t0 = w0; t0 < w1; t0 += CH) {
+    const int n = w1 - t0 < CH ? w1 - t0 : CH;
+    float2 kk[CH], vv[CH];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {  // rows past the chunk: its last row again, weighted 0
+      const int tt = t0 + (i < n ? i : n - 1);
+      const int tc = tt < T - 1 ? tt : 0;  // (row T-1 is this step's: LDS)
+      kk[i] = *reinterpret_cast<const float2*>(kb + (long long)tc * p.kvd);
+      vv[i] = *reinterpret_cast<const float2*>(vb + (long long)tc * p.kvd);
+      if (tt == T - 1) { kk[i] = kn; vv[i] = vn; }
+    }
+    float sc[CH];
+    float mc = -3.402823466e+38f;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      sc[i] = __fdiv_rn(wave_sum_u(fmaf(qv.y, kk[i].y, __fmul_rn(qv.x, kk[i].x))), rs);
+      if (i < n) mc = fmaxf(mc, sc[i]);
+    }
+    const float mn = fmaxf(m, mc);
+    const float scale = expf_libm(__fsub_rn(m, mn));  // rescale what earlier chunks summed
+    lsum = __fmul_rn(lsum, scale);
+    o.x = __fmul_rn(o.x, scale);
+    o.y = __fmul_rn(o.y, scale);
+#pragma unroll
+    for (int i = 0; i < CH; ++i)
+      if (i < n) {
+        const float e = expf_libm(__fsub_rn(sc[i], mn));
+        lsum = __fadd_rn(lsum, e);
+        o.x = fmaf(e, vv[i].x, o.x);
+        o.y = fmaf(e, vv[i].y, o.y);
+      }
+    m = mn;
+  }
+  // the waves' partial softmax states, combined in wave order
+  float* cmb = qkv + 3 * HS;  // [PW][HS + 2]
+  cmb[wave * (HS + 2) + 2 * lane] = o.x;
+  cmb[wave * (HS + 2) + 2 * lane + 1] = o.y;
+  if (lane == 0) {
+    cmb[wave * (HS + 2) + HS] = m;
+    cmb[wave * (HS + 2) + HS + 1] = lsum;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float M = -3.402823466e+38f;
+    for (int w = 0; w < PW; ++w) M = fmaxf(M, cmb[w * (HS + 2) + HS]);
+    float L = 0.f, ox = 0.f, oy = 0.f;
+    for (int w = 0; w < PW; ++w) {
+      const float lw = cmb[w * (HS + 2) + HS + 1];
+      if (lw == 0.f) continue;  // (a wave without keys)
+      const float f = expf_libm(__fsub_rn(cmb[w * (HS + 2) + HS], M));
+      L = fmaf(lw, f, L);
+      ox = fmaf(cmb[w * (HS + 2) + 2 * lane], f, ox);
+      oy = fmaf(cmb[w * (HS + 2) + 2 * lane + 1], f, oy);
+    }
+    st_gran2(rsrc_of(d.gout + (long long)b * p.dim), (unsigned)(h * HS + 2 * lane) * 8u, d.tag_out + 1,
+             __fdiv_rn(ox, L), __fdiv_rn(oy, L));
+  }
+}
+
 // Sharded-counter grid barrier (the final one only), as persist_b.hip.
 TL_DEVICE void grid_barrier(const PStep& p) {
   __syncthreads();
@@ -655,6 +807,7 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, f4* xs, float* pres, u
     const int l = ph / 5;
     const int kind = ph == nph - 1 ? PK_CLS : ph % 5;
     if constexpr (ROLE0) TRACE_K(0);
+    if (kind == PK_ATTN && attn_fusable(p)) continue;  // (ran inside the QKV phase's reduce)
     if (kind == PK_ATTN) {
       if constexpr (!ROLE0) {  // the slot buffers are empty here: say so, so they are not kept live
 #pragma unroll
@@ -714,9 +867,19 @@ TL_DEVICE void phases(const PStep& p, int wave, int lane, f4* xs, float* pres, u
       TRACE_K(4);
       if (lane == 0) *ctr = 0u;  // the next phase's slot counter (used after its staging barrier)
     }
-    reduce(d, g, p, l, xres, ssred, sscale, rcs, etab, cbest, wave, lane);
-    if constexpr (!ROLE0) {
-      if (kPrefetchAfterReduce) prefetch_next<RWD, RWH>(p, kind, l, tb, sw, lane, buf);
+    if (kind == PK_QKV && attn_fusable(p)) {
+      // (LDS scratch: the row partials, free from the sweep barrier until the next phase's sweep —
+      // the staged slice is not: the Wo staging of the faster waves would overwrite the combine)
+      reduce_qkv_attn(d, g, p, l, sscale, rcs, pres, wave, lane);
+      if constexpr (!ROLE0) {  // Wo's first slots
+        const KDesc nd = make_desc(p, PK_WO, l, tb);
+        prefetch<RWD>(nd, geo(nd), p, sw, lane, buf);
+      }
+    } else {
+      reduce(d, g, p, l, xres, ssred, sscale, rcs, etab, cbest, wave, lane);
+      if constexpr (!ROLE0) {
+        if (kPrefetchAfterReduce) prefetch_next<RWD, RWH>(p, kind, l, tb, sw, lane, buf);
+      }
     }
     if constexpr (ROLE0) TRACE_K(5);
   }
