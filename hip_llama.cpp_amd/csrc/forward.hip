@@ -364,6 +364,11 @@ extern "C" int thallama_decoder_create(thallama_decoder** out, const Config* cfg
   d->nt = wbytes > 1024.0 * 1024.0 * 1024.0;
   // persistent step: batch 1, fp32 (decided again for int8 in _create_q8)
   TL_TRY(hipDeviceGetAttribute(&d->ncu, hipDeviceAttributeMultiprocessorCount, d->dev));
+  if (batch == 1) {  // measurement only: a smaller batch-1 persistent grid (a multiple of 8 blocks)
+    const char* e = getenv("THALLAMA_PERSIST_GRID");
+    const int g = e ? atoi(e) : 0;
+    if (g >= 8 && g % 8 == 0 && g < d->ncu) d->ncu = g;
+  }
   {
     tl::PStep ps = {};
     ps.dim = d->dim; ps.hid = d->hidden; ps.kvd = d->kv_dim; ps.hs = d->hs; ps.NS = d->nsplit;
