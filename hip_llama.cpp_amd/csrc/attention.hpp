@@ -649,6 +649,10 @@ TL_DEVICE void attn_unit_split(const AttnWaveParams& w, int h, int c, int NG, fl
 // attn_unit (same records and tickets).  win: attn_win_floats(HS) floats of LDS.
 __host__ __device__ constexpr int attn_win_floats(int hs) { return 2 * 64 * hs + 2 * hs; }
 
+#ifndef ATTN_MERGE_LAST  // (0: key T-1 folded after the round; same-box A/B only)
+#define ATTN_MERGE_LAST 1
+#endif
+
 // The key range of attn_unit_win's unit (b, h, split s): [k0, k1) of T keys, the cached ones
 // [k0, ke); live = the unit has keys.
 struct WinUnit {
@@ -750,6 +754,11 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
   const unsigned long long* srck = gq + p.dim + kvh * HS;
   const unsigned long long* srcv = gq + p.dim + p.kv_dim + kvh * HS;
   const bool last = k1 == T;
+  // A single-round unit holding key T-1 takes its k / v rows as window row ke - k0 and folds all
+  // its keys in one round (one max, one rescale); a separate fold of that key after the round was
+  // one more dependent chain of LDS reads and wave reductions on the attention phase's critical path.
+  const bool merge = ATTN_MERGE_LAST && last && !multi && ke - k0 < 64;
+  float* kdst = merge ? kw + (ke - k0) * HS : kn;
   float vn[VPL];
   {
     unsigned long long g[3][VPL];
@@ -766,12 +775,15 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
       qs[lane * VPL + c] = (unsigned)(g[0][c] >> 32) == w.tag_in ? __uint_as_float((unsigned)g[0][c])
                                                                   : gran_wait(srcq + lane * VPL + c, w.tag_in, w.err, w.poll_long != 0);
       if (last) {
-        kn[lane * VPL + c] = (unsigned)(g[1][c] >> 32) == w.tag_in ? __uint_as_float((unsigned)g[1][c])
-                                                                    : gran_wait(srck + lane * VPL + c, w.tag_in, w.err, w.poll_long != 0);
+        kdst[lane * VPL + c] = (unsigned)(g[1][c] >> 32) == w.tag_in ? __uint_as_float((unsigned)g[1][c])
+                                                                      : gran_wait(srck + lane * VPL + c, w.tag_in, w.err, w.poll_long != 0);
         vn[c] = (unsigned)(g[2][c] >> 32) == w.tag_in ? __uint_as_float((unsigned)g[2][c])
                                                        : gran_wait(srcv + lane * VPL + c, w.tag_in, w.err, w.poll_long != 0);
       }
     }
+    if (merge)  // (rows 0 .. ke - k0 - 1 are the DMAs' own)
+#pragma unroll
+      for (int c = 0; c < VPL; ++c) vw[(ke - k0) * HS + lane * VPL + c] = vn[c];
   }
   wave_lds_fence();
   if (w.ts && lane == 0) w.ts[0] = __builtin_amdgcn_s_memrealtime();  // (diagnostics: q / k / v granules in)
@@ -820,11 +832,13 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
     }
     m = mn;
   };
-  for (int t0 = k0; t0 < ke; t0 += 64) {
-    const int n = min(64, ke - t0);
+  const int kend = merge ? ke + 1 : ke;  // the window's last key (merge: row ke - k0 is key T-1)
+  for (int t0 = k0; t0 < kend; t0 += 64) {
+    const int n = min(64, kend - t0);
     const bool more = t0 + 64 < ke;
     if (multi) wait_all_but_round_half();  // this round's K rows (its V rows may still be in flight)
     else dma_wait_all();
+    if (w.ts && lane == 0 && t0 == k0) w.ts[4] = __builtin_amdgcn_s_memrealtime();  // (diagnostics: first K rows in)
     float sc;
     {  // key `lane`, pieces in the order lane, lane + 1, ... (mod PC)
       float a[4] = {0.f, 0.f, 0.f, 0.f};
@@ -837,6 +851,7 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
       sc = (a[0] + a[1]) + (a[2] + a[3]);
     }
     wave_lds_fence();  // the K window's reads are done before the next round lands in it
+    if (w.ts && lane == 0 && t0 == k0) w.ts[5] = __builtin_amdgcn_s_memrealtime();  // (diagnostics: first scores)
     if (more) {
       issue_k(t0 + 64, min(64, ke - t0 - 64));
       wait_all_but_round_half();  // this round's V rows
@@ -848,7 +863,7 @@ TL_DEVICE void attn_unit_win(const AttnWaveParams& w, int unit, float* win, int 
     if (more) issue_v(t0 + 64, min(64, ke - t0 - 64));
   }
   if (w.ts && lane == 0) w.ts[1] = __builtin_amdgcn_s_memrealtime();  // (diagnostics: cached keys folded)
-  if (last) {  // key T-1: every lane computes its score (one key), lane 0's counts
+  if (last && !merge) {  // key T-1: every lane computes its score (one key), lane 0's counts
     const float sc = dot(kn, 1);
     // fold one key whose V row is vn (in registers): the same arithmetic inline
     const float my = lane < 1 ? __fdiv_rn(sc, rs) : -3.402823466e+38f;

@@ -205,8 +205,9 @@ def main():
             print(f"attention units ({int(live.sum() / len(att))} per layer): q {rel(8):.2f}  scores/kv {rel(9):.2f}  "
                   f"summed {rel(11):.2f}  computed {rel(10):.2f}  done {rel(3):.2f} us after phase start")
         else:  # attn_unit_win (fp32, batch 1): granules in, cached keys folded, computed, published
-            print(f"attention units ({int(live.sum() / len(att))} per layer): q/k/v in {rel(8):.2f}  cached keys "
-                  f"{rel(9):.2f}  computed {rel(11):.2f}  published {rel(10):.2f}  done {rel(3):.2f} us after phase start")
+            print(f"attention units ({int(live.sum() / len(att))} per layer): q/k/v in {rel(8):.2f}  first K rows in "
+                  f"{rel(12):.2f}  first scores {rel(13):.2f}  cached keys {rel(9):.2f}  computed {rel(11):.2f}  "
+                  f"published {rel(10):.2f}  done {rel(3):.2f} us after phase start")
         # the hand-offs around attention, per layer (median over layers): the last QKV epilogue's end,
         # the last head published, and the Wo staging's gather, relative to the median attention start
         qkv_end = np.stack([t[:, ph - 1, 3].max() for ph in att])
